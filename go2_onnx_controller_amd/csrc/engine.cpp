@@ -1,0 +1,594 @@
+// go2pi engine: C-ABI implementation (include/go2pi.h).
+//
+// Replaces the onnxruntime session behind ONNXActor
+// (onnx_inference/src/cpp/onnx_actor.cpp:6-48) with an MI355X-native runtime:
+//  - load: parse the .onnx with our own reader (onnx_model.cpp), lower it to a
+//    program of dense layers (+ optional GRU), pack weights once into MFMA
+//    fragment order (program.hpp) and upload them to HBM (one arena);
+//  - host path (go2pi_run): small batches replay a captured hipGraph whose
+//    kernels read the observation from / write the action to pinned,
+//    host-mapped staging (no memcpy nodes); larger batches stage through
+//    device buffers and launch the fused batched kernel;
+//  - device path (go2pi_run_device): enqueue on the caller's stream, no sync.
+// No CPU fallback exists: without a HIP device, go2pi_create fails loudly.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/go2pi.h"
+#include "onnx_model.hpp"
+#include "program.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct HipError : std::runtime_error {
+  int code;
+  HipError(const std::string &m, int c) : std::runtime_error(m), code(c) {}
+};
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw HipError(std::string("HIP error in ") + what + ": " + hipGetErrorString(e), GO2PI_E_DEVICE);
+}
+void hip_check(int e, const char *what) { hip_check(static_cast<hipError_t>(e), what); }
+
+struct ApiError : std::runtime_error {
+  int code;
+  ApiError(const std::string &m, int c) : std::runtime_error(m), code(c) {}
+};
+
+inline int ceil16(int x) { return (x + 15) & ~15; }
+
+}  // namespace
+
+struct go2pi_engine {
+  go2pi::Model model;
+  go2pi_opts opts{};
+  int device = 0;
+  int waves = 8;
+  int small_batch = 8;
+  hipStream_t stream = nullptr;
+  go2pi::DevProgram prog{};
+  std::vector<void *> allocs;  // device allocations
+  float *d_hidden = nullptr;   // [max_batch][H]
+  float *d_obs = nullptr;      // host-path staging [max_batch][in]
+  float *d_act = nullptr;      // [max_batch][out]
+  float *d_tmp[2] = {nullptr, nullptr};  // small-batch activations [SMALL_MAXB][maxw]
+  int tmp_stride = 0;
+  float *h_obs = nullptr, *h_act = nullptr;  // pinned, host-mapped
+  float *m_obs = nullptr, *m_act = nullptr;  // device aliases of the above
+  hipGraphExec_t graphs[GO2PI_SMALL_MAXB + 1] = {};
+  hipGraph_t graph_defs[GO2PI_SMALL_MAXB + 1] = {};
+  go2pi_cost cost{};
+
+  ~go2pi_engine() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (int i = 0; i <= GO2PI_SMALL_MAXB; ++i) {
+      if (graphs[i]) (void)hipGraphExecDestroy(graphs[i]);
+      if (graph_defs[i]) (void)hipGraphDestroy(graph_defs[i]);
+    }
+    for (void *p : allocs) (void)hipFree(p);
+    if (h_obs) (void)hipHostFree(h_obs);
+    if (h_act) (void)hipHostFree(h_act);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  template <class T>
+  T *dalloc(size_t count) {
+    void *p = nullptr;
+    hip_check(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
+    allocs.push_back(p);
+    return static_cast<T *>(p);
+  }
+  template <class T>
+  T *upload(const std::vector<T> &v) {
+    T *p = dalloc<T>(v.size());
+    if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+    return p;
+  }
+
+  bool use_chain(int64_t batch) const {
+    return !model.has_gru && small_batch > 0 && batch <= small_batch;
+  }
+
+  // Enqueue one forward over `batch` rows (obs/act: device-accessible pointers).
+  void enqueue(const float *obs, float *act, int64_t batch, hipStream_t s) {
+    if (use_chain(batch)) {
+      const float *x = obs;
+      int xs = prog.in_dim;
+      for (int l = 0; l < prog.nl; ++l) {
+        const bool last = l == prog.nl - 1;
+        float *y = last ? act : d_tmp[l & 1];
+        const int ys = last ? prog.out_dim : tmp_stride;
+        hip_check(go2pi::launch_gemv_layer(prog, l, x, xs, y, ys, (int)batch, s), "gemv_layer launch");
+        x = y;
+        xs = ys;
+      }
+    } else {
+      hip_check(go2pi::launch_policy_fused(prog, waves, obs, act, d_hidden, (int)batch, 1, s), "fused launch");
+    }
+  }
+
+  hipGraphExec_t graph_for(int b) {
+    if (graphs[b]) return graphs[b];
+    hip_check(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    try {
+      enqueue(m_obs, m_act, b, stream);
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(stream, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    hip_check(hipStreamEndCapture(stream, &graph_defs[b]), "hipStreamEndCapture");
+    hip_check(hipGraphInstantiate(&graphs[b], graph_defs[b], nullptr, nullptr, 0), "hipGraphInstantiate");
+    return graphs[b];
+  }
+};
+
+namespace {
+
+void pack_dense(const go2pi::Dense &d, std::vector<float> &w, std::vector<float> &b, int &K_pad, int &N_pad) {
+  K_pad = ceil16(d.K);
+  N_pad = ceil16(d.N);
+  const int T = N_pad / 16, C = K_pad / 16;
+  w.assign((size_t)T * C * 64 * 4, 0.f);
+  for (int t = 0; t < T; ++t)
+    for (int c = 0; c < C; ++c)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 4; ++j) {
+          const int n = 16 * t + (lane & 15), k = 16 * c + 4 * (lane >> 4) + j;
+          w[(((size_t)t * C + c) * 64 + lane) * 4 + j] = (n < d.N && k < d.K) ? d.W[(size_t)n * d.K + k] : 0.f;
+        }
+  b.assign(N_pad, 0.f);
+  std::copy(d.b.begin(), d.b.end(), b.begin());
+}
+
+// GRU fragments: [Ht][Cx + Ch][gate z,r,h][lane] float4 over the concatenated
+// [x (I_pad) | h (H)] axis; x chunks carry W, h chunks carry R.
+void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
+  I_pad = ceil16(g.I);
+  const int H = g.H, Ht = H / 16, Cx = I_pad / 16, Ch = H / 16, Cc = Cx + Ch;
+  w.assign((size_t)Ht * Cc * 3 * 64 * 4, 0.f);
+  for (int t = 0; t < Ht; ++t)
+    for (int c = 0; c < Cc; ++c)
+      for (int gate = 0; gate < 3; ++gate)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 4; ++j) {
+            const int unit = 16 * t + (lane & 15);
+            const int row = gate * H + unit;
+            float v = 0.f;
+            if (c < Cx) {
+              const int k = 16 * c + 4 * (lane >> 4) + j;
+              if (k < g.I) v = g.W[(size_t)row * g.I + k];
+            } else {
+              const int k = 16 * (c - Cx) + 4 * (lane >> 4) + j;
+              v = g.R[(size_t)row * H + k];
+            }
+            w[((((size_t)t * Cc + c) * 3 + gate) * 64 + lane) * 4 + j] = v;
+          }
+}
+
+void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o) {
+  go2pi_default_opts(&e.opts);
+  if (o) {
+    if (o->struct_size < (int32_t)offsetof(go2pi_opts, obs_mean))
+      throw ApiError("go2pi_opts.struct_size too small", GO2PI_E_INVALID);
+    std::memcpy(&e.opts, o, std::min<size_t>(sizeof(go2pi_opts), (size_t)o->struct_size));
+    e.opts.struct_size = sizeof(go2pi_opts);
+  }
+  if (e.opts.max_batch <= 0) e.opts.max_batch = 4096;
+  if (e.opts.max_batch > (int64_t)std::numeric_limits<int>::max() / 2)
+    throw ApiError("max_batch too large", GO2PI_E_INVALID);
+  try {
+    e.model = go2pi::parse_onnx(bytes, n);
+  } catch (const std::exception &ex) {
+    throw ApiError(ex.what(), GO2PI_E_MODEL);
+  }
+  auto &m = e.model;
+  if ((int)m.layers.size() > GO2PI_MAX_LAYERS)
+    throw ApiError("policy has more than " + std::to_string(GO2PI_MAX_LAYERS) + " dense layers", GO2PI_E_MODEL);
+  if (m.has_gru) {
+    if (m.gru.lbr != 1) throw ApiError("GRU linear_before_reset=0 is not supported yet (export with lbr=1)", GO2PI_E_MODEL);
+    if (m.gru.H % 16) throw ApiError("GRU hidden size must be a multiple of 16", GO2PI_E_MODEL);
+  }
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    throw ApiError("no HIP device available (go2pi has no CPU fallback)", GO2PI_E_DEVICE);
+  if (e.opts.device < 0 || e.opts.device >= ndev)
+    throw ApiError("device ordinal " + std::to_string(e.opts.device) + " out of range", GO2PI_E_INVALID);
+  e.device = e.opts.device;
+  hip_check(hipSetDevice(e.device), "hipSetDevice");
+  hip_check(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking), "hipStreamCreate");
+
+  e.waves = e.opts.waves == 4 ? 4 : 8;
+  e.small_batch = e.opts.small_batch == 0 ? GO2PI_SMALL_MAXB : std::min<int>(e.opts.small_batch, GO2PI_SMALL_MAXB);
+
+  go2pi::DevProgram &p = e.prog;
+  std::memset(&p, 0, sizeof(p));
+  p.nl = (int)m.layers.size();
+  p.in_dim = m.in_dim;
+  p.out_dim = m.out_dim;
+  int maxw = 0;
+  double flops = 0, wbytes = 0;
+  for (int l = 0; l < p.nl; ++l) {
+    std::vector<float> w, b;
+    int kp, np;
+    pack_dense(m.layers[l], w, b, kp, np);
+    auto &L = p.L[l];
+    L.w = e.upload(w);
+    L.bias = e.upload(b);
+    L.K_pad = kp;
+    L.N_pad = np;
+    L.N = m.layers[l].N;
+    L.act = m.layers[l].act;
+    L.alpha = m.layers[l].alpha;
+    maxw = std::max({maxw, kp, np});
+    flops += 2.0 * m.layers[l].K * m.layers[l].N;
+    wbytes += 4.0 * ((double)m.layers[l].K * m.layers[l].N + m.layers[l].N);
+  }
+  if (m.has_gru) {
+    std::vector<float> w;
+    int ip;
+    pack_gru(m.gru, w, ip);
+    const int H = m.gru.H;
+    std::vector<float> bzr(2 * H), bh(2 * H);
+    for (int j = 0; j < H; ++j) {
+      bzr[j] = m.gru.Wb[j] + m.gru.Rb[j];
+      bzr[H + j] = m.gru.Wb[H + j] + m.gru.Rb[H + j];
+      bh[j] = m.gru.Wb[2 * H + j];
+      bh[H + j] = m.gru.Rb[2 * H + j];
+    }
+    p.has_gru = 1;
+    p.gru.w = e.upload(w);
+    p.gru.bzr = e.upload(bzr);
+    p.gru.bh = e.upload(bh);
+    p.gru.I = m.gru.I;
+    p.gru.I_pad = ip;
+    p.gru.H = H;
+    p.gru.lbr = m.gru.lbr;
+    p.in_pad = ip;
+    maxw = std::max({maxw, ip, H});
+    flops += 2.0 * 3 * H * ((double)m.gru.I + H);
+    wbytes += 4.0 * (3.0 * H * (m.gru.I + H) + 6.0 * H);
+    e.d_hidden = e.dalloc<float>((size_t)e.opts.max_batch * H);
+    hip_check(hipMemset(e.d_hidden, 0, (size_t)e.opts.max_batch * H * sizeof(float)), "hipMemset");
+  } else {
+    p.in_pad = p.L[0].K_pad;
+  }
+  p.lds_stride = maxw + 4;  // +16 B per row: rows start on different LDS banks
+
+  // prologue: model-defined (Sub/Div nodes) and/or opts-defined normalisation
+  std::vector<float> sub = m.pre_sub, div = m.pre_div;
+  if (e.opts.obs_mean) {
+    if (!sub.empty()) throw ApiError("model already normalises its input; obs_mean not allowed", GO2PI_E_INVALID);
+    sub.assign(e.opts.obs_mean, e.opts.obs_mean + m.in_dim);
+  }
+  if (e.opts.obs_std) {
+    if (!div.empty()) throw ApiError("model already normalises its input; obs_std not allowed", GO2PI_E_INVALID);
+    div.assign(e.opts.obs_std, e.opts.obs_std + m.in_dim);
+  }
+  if (!sub.empty()) { p.pre_sub = e.upload(sub); p.pre_sub_bcast = sub.size() == 1; }
+  if (!div.empty()) { p.pre_div = e.upload(div); p.pre_div_bcast = div.size() == 1; }
+  p.obs_clip = e.opts.obs_clip;
+  p.post_tanh = e.opts.action_tanh ? 1 : 0;
+  p.clip_lo = m.clip_lo;
+  p.clip_hi = m.clip_hi;
+  if (e.opts.action_clip > 0.f) {
+    p.clip_lo = std::max(p.clip_lo, -e.opts.action_clip);
+    p.clip_hi = std::min(p.clip_hi, e.opts.action_clip);
+  }
+  p.scale = (e.opts.action_scale != 0.f) ? e.opts.action_scale : 1.f;
+
+  const size_t lds = go2pi::fused_lds_bytes(p, e.waves);
+  if (lds > 160 * 1024)
+    throw ApiError("layer width " + std::to_string(maxw) + " needs " + std::to_string(lds) +
+                   " B of LDS per tile (> 160 KiB)", GO2PI_E_MODEL);
+  hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
+
+  // buffers
+  e.d_obs = e.dalloc<float>((size_t)e.opts.max_batch * m.in_dim);
+  e.d_act = e.dalloc<float>((size_t)e.opts.max_batch * m.out_dim);
+  e.tmp_stride = maxw;
+  e.d_tmp[0] = e.dalloc<float>((size_t)GO2PI_SMALL_MAXB * maxw);
+  e.d_tmp[1] = e.dalloc<float>((size_t)GO2PI_SMALL_MAXB * maxw);
+  hip_check(hipHostMalloc((void **)&e.h_obs, sizeof(float) * GO2PI_SMALL_MAXB * m.in_dim,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc");
+  hip_check(hipHostMalloc((void **)&e.h_act, sizeof(float) * GO2PI_SMALL_MAXB * m.out_dim,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc");
+  hip_check(hipHostGetDevicePointer((void **)&e.m_obs, e.h_obs, 0), "hipHostGetDevicePointer");
+  hip_check(hipHostGetDevicePointer((void **)&e.m_act, e.h_act, 0), "hipHostGetDevicePointer");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+
+  e.cost.flops_per_row = flops;
+  e.cost.weight_bytes = wbytes;
+  e.cost.io_bytes_per_row = 4.0 * (m.in_dim + m.out_dim) + (m.has_gru ? 8.0 * m.gru.H : 0.0);
+  e.cost.n_layers = p.nl;
+  e.cost.has_gru = p.has_gru;
+}
+
+template <class F>
+int guarded(F &&f) {
+  try {
+    g_last_error.clear();
+    return f();
+  } catch (const ApiError &ex) {
+    g_last_error = ex.what();
+    return ex.code;
+  } catch (const HipError &ex) {
+    g_last_error = ex.what();
+    return ex.code;
+  } catch (const std::bad_alloc &) {
+    g_last_error = "out of host memory";
+    return GO2PI_E_INVALID;
+  } catch (const std::exception &ex) {
+    g_last_error = ex.what();
+    return GO2PI_E_INVALID;
+  }
+}
+
+void check_engine(const go2pi_engine *e) {
+  if (!e) throw ApiError("null engine", GO2PI_E_INVALID);
+}
+
+void check_batch(const go2pi_engine *e, int64_t batch) {
+  if (batch < 0) throw ApiError("negative batch", GO2PI_E_INVALID);
+  if (batch > e->opts.max_batch)
+    throw ApiError("batch " + std::to_string(batch) + " exceeds max_batch " + std::to_string(e->opts.max_batch),
+                   GO2PI_E_CAPACITY);
+}
+
+}  // namespace
+
+extern "C" {
+
+void go2pi_default_opts(go2pi_opts *o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->struct_size = sizeof(go2pi_opts);
+  o->device = 0;
+  o->max_batch = 4096;
+  o->use_graph = 1;
+  o->log_level = 2;
+  o->waves = 0;
+  o->small_batch = 0;
+  o->obs_clip = 0.f;
+  o->action_tanh = 0;
+  o->action_clip = 0.f;
+  o->action_scale = 0.f;
+}
+
+int go2pi_create_from_memory(const void *bytes, size_t nbytes, const go2pi_opts *opts, go2pi_engine **out) {
+  return guarded([&] {
+    if (!out) throw ApiError("null output pointer", GO2PI_E_INVALID);
+    *out = nullptr;
+    if (!bytes || !nbytes) throw ApiError("empty model buffer", GO2PI_E_MODEL);
+    auto e = std::make_unique<go2pi_engine>();
+    build(*e, static_cast<const uint8_t *>(bytes), nbytes, opts);
+    *out = e.release();
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_create(const char *path, const go2pi_opts *opts, go2pi_engine **out) {
+  return guarded([&] {
+    if (!out) throw ApiError("null output pointer", GO2PI_E_INVALID);
+    *out = nullptr;
+    if (!path) throw ApiError("null model path", GO2PI_E_INVALID);
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw ApiError(std::string("cannot open model file '") + path + "'", GO2PI_E_MODEL);
+    std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (buf.empty()) throw ApiError(std::string("empty model file '") + path + "'", GO2PI_E_MODEL);
+    auto e = std::make_unique<go2pi_engine>();
+    build(*e, buf.data(), buf.size(), opts);
+    *out = e.release();
+    return GO2PI_OK;
+  });
+}
+
+void go2pi_destroy(go2pi_engine *e) { delete e; }
+
+int go2pi_num_io(const go2pi_engine *e, int32_t *ni, int32_t *no) {
+  return guarded([&] {
+    check_engine(e);
+    if (ni) *ni = (int32_t)e->model.inputs.size();
+    if (no) *no = (int32_t)e->model.outputs.size();
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_io_name(const go2pi_engine *e, int32_t is_output, int32_t index, char *buf, size_t cap) {
+  return guarded([&] {
+    check_engine(e);
+    const auto &v = is_output ? e->model.outputs : e->model.inputs;
+    if (index < 0 || index >= (int32_t)v.size()) throw ApiError("io index out of range", GO2PI_E_INVALID);
+    if (!buf || cap == 0) throw ApiError("null name buffer", GO2PI_E_INVALID);
+    const std::string &s = v[index].name;
+    const size_t k = std::min(cap - 1, s.size());
+    std::memcpy(buf, s.data(), k);
+    buf[k] = 0;
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_io_shape(const go2pi_engine *e, int32_t is_output, int32_t index, int64_t *dims, int32_t cap,
+                   int32_t *rank) {
+  return guarded([&] {
+    check_engine(e);
+    const auto &v = is_output ? e->model.outputs : e->model.inputs;
+    if (index < 0 || index >= (int32_t)v.size()) throw ApiError("io index out of range", GO2PI_E_INVALID);
+    const auto &s = v[index].shape;
+    if (rank) *rank = (int32_t)s.size();
+    for (int32_t i = 0; dims && i < cap && i < (int32_t)s.size(); ++i) dims[i] = s[i];
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_io_dims(const go2pi_engine *e, int64_t *in_dim, int64_t *out_dim) {
+  return guarded([&] {
+    check_engine(e);
+    if (in_dim) *in_dim = e->model.in_dim;
+    if (out_dim) *out_dim = e->model.out_dim;
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
+  return guarded([&] {
+    check_engine(e);
+    check_batch(e, batch);
+    if (batch == 0) return GO2PI_OK;
+    if (!obs || !act) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    const size_t in_b = sizeof(float) * (size_t)batch * e->model.in_dim;
+    const size_t out_b = sizeof(float) * (size_t)batch * e->model.out_dim;
+    if (batch <= GO2PI_SMALL_MAXB) {
+      // pinned host-mapped staging: kernels read obs / write act over PCIe directly
+      std::memcpy(e->h_obs, obs, in_b);
+      if (e->opts.use_graph) {
+        hip_check(hipGraphLaunch(e->graph_for((int)batch), e->stream), "hipGraphLaunch");
+      } else {
+        e->enqueue(e->m_obs, e->m_act, batch, e->stream);
+      }
+      hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      std::memcpy(act, e->h_act, out_b);
+    } else {
+      hip_check(hipMemcpyAsync(e->d_obs, obs, in_b, hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync H2D");
+      e->enqueue(e->d_obs, e->d_act, batch, e->stream);
+      hip_check(hipMemcpyAsync(act, e->d_act, out_b, hipMemcpyDeviceToHost, e->stream), "hipMemcpyAsync D2H");
+      hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    }
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int64_t batch, void *hip_stream) {
+  return guarded([&] {
+    check_engine(e);
+    check_batch(e, batch);
+    if (batch == 0) return GO2PI_OK;
+    if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    e->enqueue(obs_dev, act_dev, batch, static_cast<hipStream_t>(hip_stream));
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int64_t steps, int64_t batch,
+                              void *hip_stream) {
+  return guarded([&] {
+    check_engine(e);
+    check_batch(e, batch);
+    if (steps < 0) throw ApiError("negative steps", GO2PI_E_INVALID);
+    if (batch == 0 || steps == 0) return GO2PI_OK;
+    if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
+    if ((double)steps * batch * std::max(e->model.in_dim, e->model.out_dim) > 2147483647.0 * 4)
+      throw ApiError("sequence too large", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    hip_check(go2pi::launch_policy_fused(e->prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch, (int)steps, s),
+              "fused sequence launch");
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_hidden_dim(const go2pi_engine *e, int64_t *hd) {
+  return guarded([&] {
+    check_engine(e);
+    if (hd) *hd = e->model.has_gru ? e->model.gru.H : 0;
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_reset_hidden(go2pi_engine *e, const uint8_t *mask, int64_t batch) {
+  return guarded([&] {
+    check_engine(e);
+    if (!e->model.has_gru) return GO2PI_OK;
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    const int H = e->model.gru.H;
+    if (!mask) {
+      hip_check(hipMemsetAsync(e->d_hidden, 0, sizeof(float) * (size_t)e->opts.max_batch * H, e->stream), "hipMemsetAsync");
+    } else {
+      check_batch(e, batch);
+      // coalesce runs of reset rows into single memsets
+      int64_t i = 0;
+      while (i < batch) {
+        if (!mask[i]) { ++i; continue; }
+        int64_t j = i;
+        while (j < batch && mask[j]) ++j;
+        hip_check(hipMemsetAsync(e->d_hidden + (size_t)i * H, 0, sizeof(float) * (size_t)(j - i) * H, e->stream),
+                  "hipMemsetAsync");
+        i = j;
+      }
+    }
+    hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_get_hidden(go2pi_engine *e, float *h, int64_t batch) {
+  return guarded([&] {
+    check_engine(e);
+    check_batch(e, batch);
+    if (!e->model.has_gru || batch == 0) return GO2PI_OK;
+    if (!h) throw ApiError("null hidden buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    hip_check(hipMemcpy(h, e->d_hidden, sizeof(float) * (size_t)batch * e->model.gru.H, hipMemcpyDeviceToHost),
+              "hipMemcpy D2H");
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_set_hidden(go2pi_engine *e, const float *h, int64_t batch) {
+  return guarded([&] {
+    check_engine(e);
+    check_batch(e, batch);
+    if (!e->model.has_gru || batch == 0) return GO2PI_OK;
+    if (!h) throw ApiError("null hidden buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    hip_check(hipMemcpy(e->d_hidden, h, sizeof(float) * (size_t)batch * e->model.gru.H, hipMemcpyHostToDevice),
+              "hipMemcpy H2D");
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_sync(go2pi_engine *e) {
+  return guarded([&] {
+    check_engine(e);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *c) {
+  return guarded([&] {
+    check_engine(e);
+    if (!c) throw ApiError("null cost", GO2PI_E_INVALID);
+    *c = e->cost;
+    return GO2PI_OK;
+  });
+}
+
+const char *go2pi_last_error(void) { return g_last_error.c_str(); }
+
+const char *go2pi_version(void) { return "go2pi 0.1.0 (gfx950)"; }
+
+}  // extern "C"

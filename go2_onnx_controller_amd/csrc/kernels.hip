@@ -1,0 +1,476 @@
+// HIP kernels for gfx950 (MI355X, CDNA4): the policy forward pass that the
+// reference delegates to onnxruntime's CPU EP inside ONNXActor::act()
+// (onnx_inference/src/cpp/onnx_actor.cpp:47 -> Gemm/Elu chain of model.onnx).
+//
+// 1. policy_fused_kernel<NW>  — the batched (many-robot) path.
+//    One workgroup owns a tile of 16 robots for the WHOLE policy: the
+//    activations of its 16 rows stay in LDS between layers (never touch HBM),
+//    every layer is a strict-fp32 MFMA contraction (v_mfma_f32_16x16x4_f32:
+//    A = 16 robots x 4 k from LDS, B = 4 k x 16 outputs straight from HBM/L2 in
+//    the pre-packed fragment order of program.hpp), bias enters as the
+//    accumulator's initial value, the activation is fused into the epilogue,
+//    and the final layer writes the action rows (with the optional
+//    tanh/clip/scale epilogue) directly to global memory. A recurrent policy
+//    runs its GRU cell first with the hidden rows carried in LDS across ticks.
+//    At batch 4096 the grid is exactly 256 workgroups = one per CU.
+//
+// 2. gemv_layer_kernel        — the small-batch (1..8 robots) latency path.
+//    One workgroup per 16-output tile, 8 waves split the K chunks, fp32 VALU
+//    dot products on the same packed fragments + wave/LDS reductions. One
+//    launch per layer, captured into a hipGraph by the engine.
+//
+// Numerics: fp32 storage and arithmetic throughout (the f32-input MFMA is an
+// exact k-ordered fmaf chain, no TF32/xf32 on gfx950). The summation order
+// differs from the CPU reference, so parity is tolerance-based (north_star:
+// 1e-5 fp32 vs the CPU path), while every robot row is computed with an
+// identical instruction sequence wherever it sits in the batch: sharded and
+// unsharded runs are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include "program.hpp"
+
+namespace go2pi {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float act_fn(int act, float alpha, float x) {
+  switch (act) {
+    case 1: return x > 0.f ? x : alpha * expm1f(x);            // Elu (ONNX opset 6)
+    case 2: return x > 0.f ? x : 0.f;                          // Relu
+    case 3: return tanhf(x);                                   // Tanh
+    case 4: return 1.f / (1.f + expf(-x));                     // Sigmoid
+    case 5: return x >= 0.f ? x : alpha * x;                   // LeakyRelu
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float post_fn(const DevProgram &P, float v) {
+  if (P.post_tanh) v = tanhf(v);
+  v = fminf(fmaxf(v, P.clip_lo), P.clip_hi);
+  return v * P.scale;
+}
+
+__device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
+  if (P.pre_sub) v -= P.pre_sub[P.pre_sub_bcast ? 0 : k];
+  if (P.pre_div) v /= P.pre_div[P.pre_div_bcast ? 0 : k];
+  if (P.obs_clip > 0.f) v = fminf(fmaxf(v, -P.obs_clip), P.obs_clip);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Dense contraction over k-chunks [c0, c1) for TPW consecutive 16-col tiles.
+// X: LDS activations [16][xs], W: packed fragments of this layer.
+// Tiles beyond T are clamped (their loads duplicate tile T-1, results unused),
+// keeping the unrolled load stream free of per-element branches.
+template <int TPW>
+__device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, const float4 *__restrict__ W,
+                                          int C, int t_first, int T, int c0, int c1, int lane,
+                                          f32x4 (&acc)[TPW]) {
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const float4 *wp[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = min(t_first + i, T - 1);
+    wp[i] = W + (size_t)t * C * 64 + lane;
+  }
+  if (c0 >= c1) return;
+  float4 b[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) b[i] = wp[i][c0 * 64];
+  for (int c = c0; c < c1; ++c) {
+    const int cn = min(c + 1, c1 - 1);
+    float4 bn[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) bn[i] = wp[i][cn * 64];
+    const float4 a = *reinterpret_cast<const float4 *>(xrow + c * 16);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.x, b[i].x, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.y, b[i].y, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.z, b[i].z, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.w, b[i].w, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) b[i] = bn[i];
+  }
+}
+
+template <int TPW>
+__device__ __forceinline__ void init_bias(f32x4 (&acc)[TPW], const float *__restrict__ bias, int t_first, int T,
+                                          int lane) {
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = min(t_first + i, T - 1);
+    const float bv = bias[t * 16 + (lane & 15)];
+    acc[i] = f32x4{bv, bv, bv, bv};
+  }
+}
+
+// Epilogue of a hidden layer: activation, write the 16 x 16 tile to LDS.
+// Epilogue of the final layer: activation + post, write valid rows/cols to HBM.
+template <int TPW>
+__device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW], int t_first,
+                                            int T, int lane, bool last, float *Y, int ys, float *out, int row0,
+                                            int B) {
+  const int col = lane & 15, r0 = (lane >> 4) << 2;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = t_first + i;
+    if (t >= T) continue;
+    const int n = t * 16 + col;
+    if (!last) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_fn(L.act, L.alpha, acc[i][r]);
+    } else if (n < L.N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + r0 + r;
+        if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_fn(L.act, L.alpha, acc[i][r]));
+      }
+    }
+  }
+}
+
+template <int TPW>
+__device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
+                                            int t_first, int T, int C, int lane, bool last, float *out, int row0,
+                                            int B) {
+  f32x4 acc[TPW];
+  init_bias<TPW>(acc, L.bias, t_first, T, lane);
+  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t_first, T, 0, C, lane, acc);
+  dense_store<TPW>(P, L, acc, t_first, T, lane, last, Y, xs, out, row0, B);
+}
+
+// One dense layer for the whole workgroup (NW waves). Contains barriers only in
+// the split-K branch, which every wave of the workgroup takes together.
+template <int NW>
+__device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
+                                            f32x4 *scratch, int wave, int lane, bool last, float *out, int row0,
+                                            int B) {
+  const int T = L.N_pad >> 4, C = L.K_pad >> 4;
+  if (T >= NW) {
+    // tiles split over waves, full K per wave
+    const int tpw = (T + NW - 1) / NW;
+    int t = wave * tpw;
+    const int t_end = min(t + tpw, T);
+    for (; t + 8 <= t_end; t += 8) dense_group<8>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B);
+    const int rem = t_end - t;
+    if (rem > 4) dense_group<8>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    else if (rem > 2) dense_group<4>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    else if (rem == 2) dense_group<2>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    else if (rem == 1) dense_group<1>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+  } else {
+    // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
+    const int ks = NW / T;
+    const int t = wave % T, s = wave / T;
+    f32x4 acc[1];
+    if (s == 0) init_bias<1>(acc, L.bias, t, T, lane);
+    else acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (s < ks) {
+      const int c0 = (s * C) / ks, c1 = ((s + 1) * C) / ks;
+      dense_acc<1>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t, T, c0, c1, lane, acc);
+      if (s > 0) scratch[wave * 64 + lane] = acc[0];
+    }
+    __syncthreads();
+    if (s == 0) {
+      for (int s2 = 1; s2 < ks; ++s2) acc[0] += scratch[(t + s2 * T) * 64 + lane];
+      dense_store<1>(P, L, acc, t, T, lane, last, Y, xs, out, row0, B);
+    }
+  }
+}
+
+// GRU cell (ONNX semantics, linear_before_reset = 1) for one 16-robot tile.
+// X: LDS rows [16][xs] holding x in columns [0, I_pad); Hs: LDS hidden rows
+// (stride xs). Writes h' to Y[:, 0:H]; the caller copies it back into Hs after
+// a barrier (other waves still read Hs as their MFMA A operand here).
+template <int GT>
+__device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                          int t_first, int lane) {
+  const int Cx = G.I_pad >> 4, Ch = G.H >> 4, Cc = Cx + Ch;
+  const float4 *W = reinterpret_cast<const float4 *>(G.w);
+  const int col = lane & 15, r0 = (lane >> 4) << 2;
+  f32x4 z[GT], r[GT], nx[GT], nh[GT];
+  const float4 *wp[GT];
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+    const float bz = G.bzr[j], br = G.bzr[G.H + j], bx = G.bh[j], bh = G.bh[G.H + j];
+    z[i] = f32x4{bz, bz, bz, bz};
+    r[i] = f32x4{br, br, br, br};
+    nx[i] = f32x4{bx, bx, bx, bx};
+    nh[i] = f32x4{bh, bh, bh, bh};
+    wp[i] = W + (size_t)(t_first + i) * Cc * 192 + lane;
+  }
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
+  for (int c = 0; c < Cx; ++c) {
+    const float4 a = *reinterpret_cast<const float4 *>(xrow + c * 16);
+    float4 wz[GT], wr[GT], wh[GT];
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      wz[i] = wp[i][c * 192];
+      wr[i] = wp[i][c * 192 + 64];
+      wh[i] = wp[i][c * 192 + 128];
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.x, wz[i].x, z[i]); r[i] = mfma4(a.x, wr[i].x, r[i]); nx[i] = mfma4(a.x, wh[i].x, nx[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.y, wz[i].y, z[i]); r[i] = mfma4(a.y, wr[i].y, r[i]); nx[i] = mfma4(a.y, wh[i].y, nx[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.z, wz[i].z, z[i]); r[i] = mfma4(a.z, wr[i].z, r[i]); nx[i] = mfma4(a.z, wh[i].z, nx[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.w, wz[i].w, z[i]); r[i] = mfma4(a.w, wr[i].w, r[i]); nx[i] = mfma4(a.w, wh[i].w, nx[i]);
+    }
+  }
+  for (int c = 0; c < Ch; ++c) {
+    const float4 a = *reinterpret_cast<const float4 *>(hrow + c * 16);
+    float4 wz[GT], wr[GT], wh[GT];
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      wz[i] = wp[i][(Cx + c) * 192];
+      wr[i] = wp[i][(Cx + c) * 192 + 64];
+      wh[i] = wp[i][(Cx + c) * 192 + 128];
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.x, wz[i].x, z[i]); r[i] = mfma4(a.x, wr[i].x, r[i]); nh[i] = mfma4(a.x, wh[i].x, nh[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.y, wz[i].y, z[i]); r[i] = mfma4(a.y, wr[i].y, r[i]); nh[i] = mfma4(a.y, wh[i].y, nh[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.z, wz[i].z, z[i]); r[i] = mfma4(a.z, wr[i].z, r[i]); nh[i] = mfma4(a.z, wh[i].z, nh[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      z[i] = mfma4(a.w, wz[i].w, z[i]); r[i] = mfma4(a.w, wr[i].w, r[i]); nh[i] = mfma4(a.w, wh[i].w, nh[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r0 + e;
+      const float zg = 1.f / (1.f + expf(-z[i][e]));
+      const float rg = 1.f / (1.f + expf(-r[i][e]));
+      const float hn = tanhf(nx[i][e] + rg * nh[i][e]);
+      const float ho = Hs[row * xs + j];
+      Y[row * xs + j] = (1.f - zg) * hn + zg * ho;
+    }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                         int wave, int lane) {
+  const int Ht = G.H >> 4;
+  const int tpw = (Ht + NW - 1) / NW;
+  int t = wave * tpw;
+  const int t_end = min(t + tpw, Ht);
+  for (; t + 4 <= t_end; t += 4) gru_group<4>(G, X, Hs, Y, xs, t, lane);
+  for (; t + 2 <= t_end; t += 2) gru_group<2>(G, X, Hs, Y, xs, t, lane);
+  for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
+                                                               float *__restrict__ act, float *__restrict__ hidden,
+                                                               int B, int steps) {
+  extern __shared__ float4 lds4[];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const int S = P.lds_stride;
+  float *bufA = lds;
+  float *bufB = lds + GO2PI_TILE_ROWS * S;
+  float *bufH = lds + 2 * GO2PI_TILE_ROWS * S;  // only with a GRU
+  f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
+  constexpr int NT = NW * 64;
+  const int H = P.gru.H;
+
+  if (P.has_gru) {
+    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+      const int r = e / H, k = e - r * H, row = row0 + r;
+      bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
+    }
+  }
+  for (int step = 0; step < steps; ++step) {
+    const float *ob = obs + (size_t)step * B * P.in_dim;
+    float *ac = act + (size_t)step * B * P.out_dim;
+    for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
+      const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
+      float v = 0.f;
+      if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
+      bufA[r * S + k] = v;
+    }
+    __syncthreads();
+    float *X = bufA, *Y = bufB;
+    if (P.has_gru) {
+      gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
+      __syncthreads();
+      for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+        const int r = e / H, k = e - r * H;
+        bufH[r * S + k] = bufB[r * S + k];
+      }
+      X = bufB;
+      Y = bufA;
+      // no barrier needed: layer 0 below reads bufB (X) and writes bufA (Y); bufH is
+      // next read after the end-of-step barrier
+    }
+    for (int l = 0; l < P.nl; ++l) {
+      const bool last = l == P.nl - 1;
+      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, row0, B);
+      __syncthreads();
+      float *t = X;
+      X = Y;
+      Y = t;
+    }
+  }
+  if (P.has_gru) {
+    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+      const int r = e / H, k = e - r * H, row = row0 + r;
+      if (row < B) hidden[(size_t)row * H + k] = bufH[r * S + k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small-batch GEMV layer. grid = N_pad/16 workgroups (one per 16-output tile),
+// 8 waves split the K chunks. x: [B][x_stride] (device or host-mapped memory),
+// y: [B][y_stride]. Layer 0 applies the prologue; the final layer the epilogue.
+constexpr int GEMV_WAVES = 8;
+
+__global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram P, int layer, const float *x,
+                                                                     int x_stride, float *y, int y_stride, int B) {
+  extern __shared__ float4 lds4[];
+  float *xs = reinterpret_cast<float *>(lds4);  // [B][K_pad]
+  const DevLayer &L = P.L[layer];
+  const int K_pad = L.K_pad, C = K_pad >> 4, T = L.N_pad >> 4;
+  const int K = layer == 0 ? P.in_dim : P.L[layer - 1].N;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = blockIdx.x;
+  float *part = xs + GO2PI_SMALL_MAXB * K_pad;  // [GEMV_WAVES][B][16]
+  for (int e = tid; e < B * K_pad; e += GEMV_WAVES * 64) {
+    const int b = e / K_pad, k = e - b * K_pad;
+    float v = 0.f;
+    if (k < K) {
+      v = x[(size_t)b * x_stride + k];
+      if (layer == 0) v = prologue(P, v, k);
+    }
+    xs[b * K_pad + k] = v;
+  }
+  __syncthreads();
+  float p[GO2PI_SMALL_MAXB];
+#pragma unroll
+  for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
+  const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)t * C * 64 + lane;
+  const int koff = (lane >> 4) << 2;
+  for (int c = wave; c < C; c += GEMV_WAVES) {
+    const float4 w = W[c * 64];
+#pragma unroll
+    for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+      if (b < B) {
+        const float4 a = *reinterpret_cast<const float4 *>(xs + b * K_pad + c * 16 + koff);
+        p[b] = fmaf(a.x, w.x, p[b]);
+        p[b] = fmaf(a.y, w.y, p[b]);
+        p[b] = fmaf(a.z, w.z, p[b]);
+        p[b] = fmaf(a.w, w.w, p[b]);
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+    p[b] += __shfl_xor(p[b], 16);
+    p[b] += __shfl_xor(p[b], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int b = 0; b < GO2PI_SMALL_MAXB; ++b)
+      if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
+  }
+  __syncthreads();
+  if (wave == 0 && lane < 16) {
+    const int n = t * 16 + lane;
+    const bool last = layer == P.nl - 1;
+    const float bv = L.bias[n];
+    for (int b = 0; b < B; ++b) {
+      float s = 0.f;
+      for (int w2 = 0; w2 < GEMV_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
+      float v = act_fn(L.act, L.alpha, s + bv);
+      if (last) {
+        if (n < L.N) y[(size_t)b * y_stride + n] = post_fn(P, v);
+      } else {
+        y[(size_t)b * y_stride + n] = v;  // padded columns are exact zeros
+      }
+    }
+  }
+  (void)T;
+}
+
+// ---------------------------------------------------------------------------
+size_t fused_lds_bytes(const DevProgram &p, int waves) {
+  return sizeof(float) * (size_t)(2 + p.has_gru) * GO2PI_TILE_ROWS * p.lds_stride + sizeof(f32x4) * 64 * waves;
+}
+
+size_t gemv_lds_bytes(const DevProgram &p, int layer) {
+  return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
+}
+
+int configure_kernels(const DevProgram &p, int waves) {
+  hipError_t e = hipSuccess;
+  const int bytes = (int)fused_lds_bytes(p, waves);
+  if (waves == 8)
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<8>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  else
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<4>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) return (int)e;
+  int gmax = 0;
+  for (int l = 0; l < p.nl; ++l) gmax = std::max(gmax, (int)gemv_lds_bytes(p, l));
+  e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gemv_layer_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, gmax);
+  return (int)e;
+}
+
+int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float *act, float *hidden, int batch,
+                        int steps, void *stream) {
+  if (batch <= 0 || steps <= 0) return 0;
+  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
+  const size_t lds = fused_lds_bytes(p, waves);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (waves == 8)
+    hipLaunchKernelGGL(policy_fused_kernel<8>, grid, dim3(512), lds, s, p, obs, act, hidden, batch, steps);
+  else
+    hipLaunchKernelGGL(policy_fused_kernel<4>, grid, dim3(256), lds, s, p, obs, act, hidden, batch, steps);
+  return (int)hipGetLastError();
+}
+
+int launch_gemv_layer(const DevProgram &p, int layer, const float *x, int x_stride, float *y, int y_stride,
+                      int batch, void *stream) {
+  if (batch <= 0) return 0;
+  if (batch > GO2PI_SMALL_MAXB) return (int)hipErrorInvalidValue;
+  const dim3 grid(p.L[layer].N_pad >> 4);
+  hipLaunchKernelGGL(gemv_layer_kernel, grid, dim3(GEMV_WAVES * 64), gemv_lds_bytes(p, layer),
+                     reinterpret_cast<hipStream_t>(stream), p, layer, x, x_stride, y, y_stride, batch);
+  return (int)hipGetLastError();
+}
+
+}  // namespace go2pi

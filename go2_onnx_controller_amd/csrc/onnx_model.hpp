@@ -1,0 +1,59 @@
+// ONNX policy loader: a minimal protobuf reader plus a pattern matcher that
+// lowers an exported policy graph to the engine's program (dense layers with a
+// fused activation, optional leading GRU, optional affine prologue and clip
+// epilogue). Replaces what the reference gets from onnxruntime's session
+// creation (onnx_inference/src/cpp/onnx_actor.cpp:16, :23-28).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <limits>
+#include <string>
+#include <vector>
+
+namespace go2pi {
+
+enum Act : int { ACT_NONE = 0, ACT_ELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4, ACT_LEAKY = 5 };
+
+struct Dense {
+  int K = 0, N = 0;
+  std::vector<float> W;  // [N][K] row-major (ONNX Gemm transB=1 layout)
+  std::vector<float> b;  // [N]
+  int act = ACT_NONE;
+  float alpha = 0.f;
+};
+
+// ONNX GRU (opset 14), forward, layout 0, one layer; gates ordered z, r, h.
+struct Gru {
+  int I = 0, H = 0;
+  int lbr = 0;               // linear_before_reset
+  std::vector<float> W;      // [3H][I]
+  std::vector<float> R;      // [3H][H]
+  std::vector<float> Wb, Rb; // [3H] each
+};
+
+struct IoInfo {
+  std::string name;
+  std::vector<int64_t> shape;  // -1 for symbolic dims
+};
+
+struct Model {
+  std::vector<IoInfo> inputs, outputs;
+  int64_t ir_version = 0, opset = 0;
+  std::string producer;
+
+  // program
+  std::vector<float> pre_sub, pre_div;  // optional prologue (x - sub) / div, [in_dim]
+  bool has_gru = false;
+  Gru gru;
+  std::vector<Dense> layers;
+  float clip_lo = -std::numeric_limits<float>::infinity();
+  float clip_hi = std::numeric_limits<float>::infinity();
+  int in_dim = 0, out_dim = 0;
+};
+
+// Throws std::runtime_error with a descriptive message on malformed or
+// unsupported graphs.
+Model parse_onnx(const uint8_t *data, size_t n);
+
+}  // namespace go2pi

@@ -1,0 +1,66 @@
+// Device-side description of a loaded policy ("program"), passed to the HIP
+// kernels by value. Shared by engine.cpp (builds it) and kernels.hip (runs it).
+//
+// Weight layout in HBM ("fragment order", built once at load time):
+// a dense layer W[N][K] (ONNX Gemm transB=1 layout) is zero-padded to
+// N_pad = ceil16(N), K_pad = ceil16(K) and stored as
+//     packed[t][c][lane] : float4,  t < N_pad/16, c < K_pad/16, lane < 64
+//     packed[t][c][lane].j = W[16t + (lane & 15)][16c + 4(lane >> 4) + j]
+// so one wave-instruction (64 lanes x 16 B) reads 1 KiB of contiguous HBM and
+// the float4 feeds four v_mfma_f32_16x16x4_f32 as the B operand (B[k][n] =
+// W[n][k]) — see kernels.hip. The GRU gates use the same idea with three gate
+// fragments per (tile, chunk).
+#pragma once
+
+#include <cstdint>
+
+#define GO2PI_MAX_LAYERS 8
+#define GO2PI_TILE_ROWS 16      // robots per workgroup tile in the batched kernel
+#define GO2PI_SMALL_MAXB 8      // max rows of the GEMV chain
+
+namespace go2pi {
+
+struct DevLayer {
+  const float *w;     // packed fragments (float4 granules), see above
+  const float *bias;  // [N_pad], zero padded
+  int K_pad, N_pad, N;
+  int act;
+  float alpha;
+  int pad0, pad1, pad2;
+};
+
+struct DevGru {
+  const float *w;    // packed [Ht][Cx + Ch][3 gates][64] float4
+  const float *bzr;  // [2H]: Wb_z + Rb_z | Wb_r + Rb_r
+  const float *bh;   // [2H]: Wb_h | Rb_h
+  int I, I_pad, H, lbr;
+};
+
+struct DevProgram {
+  int nl;
+  int in_dim, in_pad, out_dim;
+  int lds_stride;  // floats per row of an LDS activation buffer
+  int has_gru;
+  // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
+  const float *pre_sub;
+  const float *pre_div;
+  int pre_sub_bcast, pre_div_bcast;  // 1: single scalar broadcast over features
+  float obs_clip;                    // <= 0: off
+  // epilogue on the final layer: y <- scale * clamp(tanh?(act(y)), lo, hi)
+  int post_tanh;
+  float clip_lo, clip_hi, scale;
+  DevGru gru;
+  DevLayer L[GO2PI_MAX_LAYERS];
+};
+
+// Host-side launchers (kernels.hip). All launches are asynchronous on `stream`.
+// Return a hipError_t as int.
+int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float *act, float *hidden, int batch,
+                        int steps, void *stream);
+size_t fused_lds_bytes(const DevProgram &p, int waves);
+int launch_gemv_layer(const DevProgram &p, int layer, const float *x, int x_stride, float *y, int y_stride,
+                      int batch, void *stream);
+size_t gemv_lds_bytes(const DevProgram &p, int layer);
+int configure_kernels(const DevProgram &p, int waves);
+
+}  // namespace go2pi

@@ -1,0 +1,267 @@
+"""ctypes binding of the go2pi C ABI (include/go2pi.h) -> `Engine`.
+
+The shared library is built in-tree (go2_onnx_controller_amd/lib/libgo2pi.so,
+see __graft_entry__.build()). There is deliberately NO CPU fallback: if the
+library or a HIP device is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgo2pi.so")
+ACTOR_LIB_PATH = os.path.join(LIB_DIR, "libonnx_actor.so")
+
+# every symbol include/go2pi.h declares (tests check the .so exports them all)
+EXPORTS = [
+    "go2pi_default_opts", "go2pi_create", "go2pi_create_from_memory", "go2pi_destroy", "go2pi_num_io",
+    "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
+    "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
+    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_last_error", "go2pi_version",
+]
+
+GO2PI_OK = 0
+ERRORS = {-1: "GO2PI_E_INVALID", -2: "GO2PI_E_MODEL", -3: "GO2PI_E_DEVICE", -4: "GO2PI_E_CAPACITY"}
+
+
+class Go2piError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("max_batch", ctypes.c_int64),
+        ("use_graph", ctypes.c_int32),
+        ("log_level", ctypes.c_int32),
+        ("waves", ctypes.c_int32),
+        ("small_batch", ctypes.c_int32),
+        ("obs_mean", ctypes.c_void_p),
+        ("obs_std", ctypes.c_void_p),
+        ("obs_clip", ctypes.c_float),
+        ("action_tanh", ctypes.c_int32),
+        ("action_clip", ctypes.c_float),
+        ("action_scale", ctypes.c_float),
+    ]
+
+
+class Cost(ctypes.Structure):
+    _fields_ = [
+        ("flops_per_row", ctypes.c_double),
+        ("weight_bytes", ctypes.c_double),
+        ("io_bytes_per_row", ctypes.c_double),
+        ("n_layers", ctypes.c_int32),
+        ("has_gru", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load libgo2pi.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        # Share ONE HIP runtime with PyTorch: torch bundles its own libamdhip64.so
+        # (same SONAME). Loading torch first makes our NEEDED libamdhip64.so.7 bind to
+        # it, so torch streams / device pointers are valid handles for go2pi.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        sig = {
+            "go2pi_default_opts": (None, [P]),
+            "go2pi_create": (ctypes.c_int, [ctypes.c_char_p, P, P]),
+            "go2pi_create_from_memory": (ctypes.c_int, [P, ctypes.c_size_t, P, P]),
+            "go2pi_destroy": (None, [P]),
+            "go2pi_num_io": (ctypes.c_int, [P, P, P]),
+            "go2pi_io_name": (ctypes.c_int, [P, I32, I32, ctypes.c_char_p, ctypes.c_size_t]),
+            "go2pi_io_shape": (ctypes.c_int, [P, I32, I32, P, I32, P]),
+            "go2pi_io_dims": (ctypes.c_int, [P, P, P]),
+            "go2pi_run": (ctypes.c_int, [P, P, P, I64]),
+            "go2pi_run_device": (ctypes.c_int, [P, P, P, I64, P]),
+            "go2pi_run_sequence_device": (ctypes.c_int, [P, P, P, I64, I64, P]),
+            "go2pi_reset_hidden": (ctypes.c_int, [P, P, I64]),
+            "go2pi_get_hidden": (ctypes.c_int, [P, P, I64]),
+            "go2pi_set_hidden": (ctypes.c_int, [P, P, I64]),
+            "go2pi_hidden_dim": (ctypes.c_int, [P, P]),
+            "go2pi_sync": (ctypes.c_int, [P]),
+            "go2pi_get_cost": (ctypes.c_int, [P, P]),
+            "go2pi_last_error": (ctypes.c_char_p, []),
+            "go2pi_version": (ctypes.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != GO2PI_OK:
+        raise Go2piError(rc, lib().go2pi_last_error().decode(errors="replace"))
+
+
+def _f32(a, n=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if n is not None and a.size != n:
+        raise ValueError(f"expected {n} floats, got {a.size}")
+    return a
+
+
+class Engine:
+    """One loaded policy on one GPU. Not thread-safe per instance (like ONNXActor)."""
+
+    def __init__(self, model, device=0, max_batch=4096, use_graph=True, waves=0, small_batch=0,
+                 obs_mean=None, obs_std=None, obs_clip=0.0, action_tanh=False, action_clip=0.0,
+                 action_scale=0.0, log_level=2):
+        L = lib()
+        o = Opts()
+        L.go2pi_default_opts(ctypes.byref(o))
+        o.device, o.max_batch, o.use_graph = int(device), int(max_batch), int(bool(use_graph))
+        o.waves, o.small_batch, o.log_level = int(waves), int(small_batch), int(log_level)
+        self._keep = []
+        if obs_mean is not None:
+            m = _f32(obs_mean)
+            self._keep.append(m)
+            o.obs_mean = m.ctypes.data
+        if obs_std is not None:
+            s = _f32(obs_std)
+            self._keep.append(s)
+            o.obs_std = s.ctypes.data
+        o.obs_clip, o.action_tanh = float(obs_clip), int(bool(action_tanh))
+        o.action_clip, o.action_scale = float(action_clip), float(action_scale)
+        h = ctypes.c_void_p()
+        if isinstance(model, (bytes, bytearray)):
+            buf = bytes(model)
+            _check(L.go2pi_create_from_memory(buf, len(buf), ctypes.byref(o), ctypes.byref(h)))
+        else:
+            _check(L.go2pi_create(os.fsencode(model), ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.max_batch = int(max_batch)
+        i, j = ctypes.c_int64(), ctypes.c_int64()
+        _check(L.go2pi_io_dims(h, ctypes.byref(i), ctypes.byref(j)))
+        self.in_dim, self.out_dim = i.value, j.value
+        hd = ctypes.c_int64()
+        _check(L.go2pi_hidden_dim(h, ctypes.byref(hd)))
+        self.hidden_dim = hd.value
+        ni, no = ctypes.c_int32(), ctypes.c_int32()
+        _check(L.go2pi_num_io(h, ctypes.byref(ni), ctypes.byref(no)))
+        self.inputs = [self._io(0, k) for k in range(ni.value)]
+        self.outputs = [self._io(1, k) for k in range(no.value)]
+        c = Cost()
+        _check(L.go2pi_get_cost(h, ctypes.byref(c)))
+        self.cost = {"flops_per_row": c.flops_per_row, "weight_bytes": c.weight_bytes,
+                     "io_bytes_per_row": c.io_bytes_per_row, "n_layers": c.n_layers, "has_gru": bool(c.has_gru)}
+
+    def _io(self, is_out, k):
+        L = lib()
+        buf = ctypes.create_string_buffer(512)
+        _check(L.go2pi_io_name(self._h, is_out, k, buf, 512))
+        dims = (ctypes.c_int64 * 8)()
+        rank = ctypes.c_int32()
+        _check(L.go2pi_io_shape(self._h, is_out, k, dims, 8, ctypes.byref(rank)))
+        return buf.value.decode(), [dims[d] for d in range(min(rank.value, 8))]
+
+    # ----------------------------------------------------------- host path
+    def run(self, obs, out=None):
+        """obs [B, in_dim] (host) -> action [B, out_dim] float32 (host)."""
+        x = _f32(obs)
+        if x.ndim == 1:
+            x = x.reshape(1, -1)
+        if x.shape[-1] != self.in_dim:
+            raise ValueError(f"observation feature dim {x.shape[-1]} != {self.in_dim}")
+        B = x.shape[0]
+        if out is None:
+            out = np.empty((B, self.out_dim), np.float32)
+        if not (out.flags.c_contiguous and out.dtype == np.float32 and out.size == B * self.out_dim):
+            raise ValueError("out must be a C-contiguous float32 array of [B, out_dim]")
+        _check(lib().go2pi_run(self._h, x.ctypes.data, out.ctypes.data, B))
+        return out
+
+    def run_ptr(self, obs_ptr, act_ptr, batch):
+        """Host pointers, as ONNXActor::act() binds them (zero-copy aliasing)."""
+        _check(lib().go2pi_run(self._h, obs_ptr, act_ptr, int(batch)))
+
+    # --------------------------------------------------------- device path
+    def run_device(self, obs_ptr, act_ptr, batch, stream=None):
+        _check(lib().go2pi_run_device(self._h, obs_ptr, act_ptr, int(batch), stream))
+
+    def run_sequence_device(self, obs_ptr, act_ptr, steps, batch, stream=None):
+        _check(lib().go2pi_run_sequence_device(self._h, obs_ptr, act_ptr, int(steps), int(batch), stream))
+
+    def run_torch(self, obs, out=None, stream=None):
+        """torch device tensors (on this engine's GPU): obs [B, in] -> act [B, out].
+        Enqueued on torch's current stream unless `stream` (a torch.cuda.Stream) is given."""
+        import torch
+        if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.device.type != "cuda":
+            raise ValueError("obs must be a contiguous float32 CUDA/HIP tensor")
+        B = obs.shape[0]
+        if out is None:
+            out = torch.empty((B, self.out_dim), dtype=torch.float32, device=obs.device)
+        s = (stream or torch.cuda.current_stream(obs.device)).cuda_stream
+        self.run_device(obs.data_ptr(), out.data_ptr(), B, s)
+        return out
+
+    def run_sequence_torch(self, obs, out=None, stream=None):
+        import torch
+        T, B = obs.shape[0], obs.shape[1]
+        if out is None:
+            out = torch.empty((T, B, self.out_dim), dtype=torch.float32, device=obs.device)
+        s = (stream or torch.cuda.current_stream(obs.device)).cuda_stream
+        self.run_sequence_device(obs.data_ptr(), out.data_ptr(), T, B, s)
+        return out
+
+    # ------------------------------------------------------ recurrent state
+    def reset_hidden(self, mask=None, batch=None):
+        if mask is None:
+            _check(lib().go2pi_reset_hidden(self._h, None, 0))
+        else:
+            m = np.ascontiguousarray(mask, dtype=np.uint8)
+            _check(lib().go2pi_reset_hidden(self._h, m.ctypes.data, m.size if batch is None else batch))
+
+    def get_hidden(self, batch):
+        h = np.empty((batch, self.hidden_dim), np.float32)
+        _check(lib().go2pi_get_hidden(self._h, h.ctypes.data, batch))
+        return h
+
+    def set_hidden(self, h):
+        h = _f32(h).reshape(-1, self.hidden_dim)
+        _check(lib().go2pi_set_hidden(self._h, h.ctypes.data, h.shape[0]))
+
+    def sync(self):
+        _check(lib().go2pi_sync(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().go2pi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def version():
+    return lib().go2pi_version().decode()

@@ -1,0 +1,147 @@
+"""Deterministic synthetic policies named by BASELINE.json's configs.
+
+BASELINE.json quotes its metric on a "48-obs -> 3x512 MLP -> 12 actions" Go2
+policy and a "GRU hidden 256" recurrent policy; neither ships with the
+reference (which only has the 98->128^3->12 model). They are
+generated here from a counter-based hash (splitmix64 of seed/tensor/element),
+PyTorch-style U(-1/sqrt(fan_in), 1/sqrt(fan_in)) init, and written as .onnx
+with our own writer. Same seed -> same bytes on any machine (sha256 pinned in
+tests/golden/synth_hashes.json).
+
+Model specs:
+  go2_mlp_512 : observation[batch,48] -> Gemm(512)+Elu -> Gemm(512)+Elu ->
+                Gemm(512)+Elu -> Gemm(12) -> action[batch,12]
+  go2_gru_256 : observation[batch,48], h_in[1,batch,256] ->
+                Unsqueeze -> GRU(H=256, linear_before_reset=1) -> Squeeze ->
+                256->512^3->12 Elu head -> action[batch,12], h_out[1,batch,256]
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+
+import numpy as np
+
+from . import onnx_writer as ow
+
+_M1 = np.uint64(0x9E3779B97F4A7C15)
+_M2 = np.uint64(0xBF58476D1CE4E5B9)
+_M3 = np.uint64(0x94D049BB133111EB)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + _M1
+        z = (z ^ (z >> np.uint64(30))) * _M2
+        z = (z ^ (z >> np.uint64(27))) * _M3
+        return z ^ (z >> np.uint64(31))
+
+
+def uniform(seed: int, tensor_id: int, shape, bound: float) -> np.ndarray:
+    """U(-bound, bound) float32, element i = f(splitmix64(seed, tensor_id, i))."""
+    n = int(np.prod(shape)) if len(shape) else 1
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0xD1B54A32D192ED03) + np.uint64(tensor_id) * np.uint64(0x8CB92BA72F3D8DD7)
+        key = base + np.arange(n, dtype=np.uint64)
+    u = (_splitmix64(key) >> np.uint64(40)).astype(np.float64) / float(1 << 24)  # [0,1)
+    return ((2.0 * u - 1.0) * bound).astype(np.float32).reshape(shape)
+
+
+def mlp_layers(dims, seed=0, first_tid=0):
+    layers = []
+    tid = first_tid
+    for k, n in zip(dims[:-1], dims[1:]):
+        bound = 1.0 / np.sqrt(k)
+        W = uniform(seed, tid, (n, k), bound)
+        b = uniform(seed, tid + 1, (n,), bound)
+        tid += 2
+        layers.append((W, b))
+    return layers
+
+
+def mlp_model_bytes(dims=(48, 512, 512, 512, 12), seed=0, act="Elu", batch="batch") -> bytes:
+    layers = mlp_layers(dims, seed)
+    nodes, inits = [], []
+    cur = "observation"
+    for i, (W, b) in enumerate(layers):
+        wn, bn = f"{2 * i}.weight", f"{2 * i}.bias"
+        inits += [(wn, W), (bn, b)]
+        last = i == len(layers) - 1
+        out = "action" if last else f"/{2 * i}/Gemm_output_0"
+        nodes.append(ow.node("Gemm", [cur, wn, bn], [out], f"/{2 * i}/Gemm",
+                             [ow.attr_float("alpha", 1.0), ow.attr_float("beta", 1.0), ow.attr_int("transB", 1)]))
+        cur = out
+        if not last:
+            aout = f"/{2 * i + 1}/{act}_output_0"
+            attrs = [ow.attr_float("alpha", 1.0)] if act == "Elu" else []
+            nodes.append(ow.node(act, [cur], [aout], f"/{2 * i + 1}/{act}", attrs))
+            cur = aout
+    return ow.model(nodes, inits, [("observation", [batch, dims[0]])], [("action", [batch, dims[-1]])])
+
+
+def gru_params(I=48, H=256, seed=0):
+    bound = 1.0 / np.sqrt(H)
+    W = uniform(seed, 100, (1, 3 * H, I), bound)
+    R = uniform(seed, 101, (1, 3 * H, H), bound)
+    B = uniform(seed, 102, (1, 6 * H), bound)
+    return W, R, B
+
+
+def gru_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch") -> bytes:
+    W, R, B = gru_params(I, H, seed)
+    layers = mlp_layers((H,) + tuple(head), seed, first_tid=200)
+    axes = np.array([0], np.int64)
+    inits = [("gru.W", W), ("gru.R", R), ("gru.B", B), ("axes0", axes)]
+    nodes = [
+        ow.node("Unsqueeze", ["observation", "axes0"], ["x_seq"], "/gru/Unsqueeze"),
+        ow.node("GRU", ["x_seq", "gru.W", "gru.R", "gru.B", "", "h_in"], ["gru_Y", "h_out"], "/gru/GRU",
+                [ow.attr_int("hidden_size", H), ow.attr_int("linear_before_reset", 1)]),
+        ow.node("Squeeze", ["h_out", "axes0"], ["h_t"], "/gru/Squeeze"),
+    ]
+    cur = "h_t"
+    for i, (Wl, bl) in enumerate(layers):
+        wn, bn = f"head.{i}.weight", f"head.{i}.bias"
+        inits += [(wn, Wl), (bn, bl)]
+        last = i == len(layers) - 1
+        out = "action" if last else f"/head/{i}/Gemm_output_0"
+        nodes.append(ow.node("Gemm", [cur, wn, bn], [out], f"/head/{i}/Gemm",
+                             [ow.attr_float("alpha", 1.0), ow.attr_float("beta", 1.0), ow.attr_int("transB", 1)]))
+        cur = out
+        if not last:
+            aout = f"/head/{i}/Elu_output_0"
+            nodes.append(ow.node("Elu", [cur], [aout], f"/head/{i}/Elu", [ow.attr_float("alpha", 1.0)]))
+            cur = aout
+    return ow.model(nodes, inits,
+                    [("observation", [batch, I]), ("h_in", [1, batch, H])],
+                    [("action", [batch, head[-1]]), ("h_out", [1, batch, H])])
+
+
+MODELS = {
+    "go2_mlp_512": lambda: mlp_model_bytes(),
+    "go2_gru_256": lambda: gru_model_bytes(),
+    # small variants for fast tests
+    "mlp_small_relu": lambda: mlp_model_bytes((20, 64, 40, 5), seed=3, act="Relu"),
+    "mlp_small_tanh": lambda: mlp_model_bytes((33, 48, 7), seed=4, act="Tanh"),
+    "gru_small": lambda: gru_model_bytes(I=10, H=32, head=(64, 6), seed=5),
+}
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODEL_DIR = os.path.join(_REPO, "build", "models")
+
+
+def ensure_model(name: str, directory: str | None = None) -> str:
+    """Write (if absent or stale) and return the path of synthetic model `name`."""
+    directory = directory or MODEL_DIR
+    os.makedirs(directory, exist_ok=True)
+    data = MODELS[name]()
+    path = os.path.join(directory, name + ".onnx")
+    if not os.path.exists(path) or open(path, "rb").read() != data:
+        tmp = path + f".tmp{os.getpid()}"
+        with open(tmp, "wb") as fh:
+            fh.write(data)
+        os.replace(tmp, path)
+    return path
+
+
+def sha256(name: str) -> str:
+    return hashlib.sha256(MODELS[name]()).hexdigest()

@@ -1,0 +1,131 @@
+/*
+ * go2pi — MI355X-native batched policy-inference engine, C ABI.
+ *
+ * This is the boundary the drop-in `ONNXActor` (include/onnx_actor.hpp) and any
+ * FFI (ctypes, cgo, JNI …) bind to. Plain pointers and sizes only; no HIP or
+ * torch types in any signature (a HIP stream travels as `void*`).
+ *
+ * Each entry point replaces one piece of the reference's onnxruntime-backed
+ * operator (inria-paris-robotics-lab/go2_onnx_controller):
+ *
+ *   go2pi_create        <- ONNXActor::ONNXActor  onnx_inference/src/cpp/onnx_actor.cpp:6-36
+ *                          (Ort::Session(env, path, SessionOptions{nullptr}) :16,
+ *                           input/output name+shape discovery :23-28)
+ *   go2pi_io_name /
+ *   go2pi_io_shape      <- GetInputNameAllocated / GetInputTypeInfo … GetShape  onnx_actor.cpp:23-28
+ *                          (consumed by print_model_info :60-66 and check_dims :50-58)
+ *   go2pi_run           <- ONNXActor::act()  onnx_actor.cpp:38-48 (Session::Run :47),
+ *                          generalised to a batch of robots (rows)
+ *   go2pi_run_device    <- same, device-resident obs/action (many-robot path)
+ *   go2pi_reset_hidden  <- (build-defined, recurrent policies)
+ *   go2pi_last_error    <- Ort::Exception::what()  (the reference throws; the C ABI returns a
+ *                          status and the C++ shim rethrows std::runtime_error)
+ *   go2pi_destroy       <- ~ONNXActor  onnx_actor.hpp:38
+ *
+ * Return codes: 0 = OK, negative = error (message via go2pi_last_error(), per
+ * thread). An engine instance is NOT re-entrant: one call at a time, exactly as
+ * the reference binds fixed tensors per ONNXActor (onnx_actor.cpp:31-35).
+ */
+#ifndef GO2PI_H_
+#define GO2PI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GO2PI_OK 0
+#define GO2PI_E_INVALID (-1)   /* bad argument */
+#define GO2PI_E_MODEL (-2)     /* unreadable / unsupported ONNX model */
+#define GO2PI_E_DEVICE (-3)    /* no HIP device / HIP runtime error */
+#define GO2PI_E_CAPACITY (-4)  /* batch above the engine's capacity */
+
+typedef struct go2pi_engine go2pi_engine;
+
+/* Engine options. Zero-initialise, then call go2pi_default_opts(). */
+typedef struct go2pi_opts {
+  int32_t struct_size;   /* = sizeof(go2pi_opts) */
+  int32_t device;        /* HIP device ordinal, default 0 */
+  int64_t max_batch;     /* robots per call capacity (device buffers), default 4096 */
+  int32_t use_graph;     /* 1 (default): the small-batch host path replays a captured hipGraph */
+  int32_t log_level;     /* OrtLoggingLevel-compatible: 0 VERBOSE … 4 FATAL, default 2 */
+  int32_t waves;         /* waves per workgroup of the batched kernel: 4 or 8 (0 = auto) */
+  int32_t small_batch;   /* host batches <= this use the GEMV chain (0 = auto: 8; -1 = never) */
+  /* Optional fused prologue / epilogue (north_star: obs normalisation, action tanh/clip).
+     All OFF by default so act() stays comparable to the shipped graph. */
+  const float *obs_mean; /* [in_dim] or NULL */
+  const float *obs_std;  /* [in_dim] or NULL: x <- (x - mean) / std */
+  float obs_clip;        /* > 0: clamp normalised obs to [-obs_clip, obs_clip] */
+  int32_t action_tanh;   /* 1: action <- tanh(action) */
+  float action_clip;     /* > 0: clamp action to [-action_clip, action_clip]
+                            (the caller's kActionLimit clamp, controller.cpp:217-223) */
+  float action_scale;    /* != 0 and != 1: action <- action * action_scale (after clip) */
+} go2pi_opts;
+
+void go2pi_default_opts(go2pi_opts *opts);
+
+/* Load an ONNX policy (Gemm/MatMul+Add with Elu/Relu/Tanh/Sigmoid/LeakyRelu, optional GRU)
+   and upload it to the device. `opts` may be NULL (defaults). */
+int go2pi_create(const char *onnx_path, const go2pi_opts *opts, go2pi_engine **out);
+int go2pi_create_from_memory(const void *onnx_bytes, size_t nbytes, const go2pi_opts *opts,
+                             go2pi_engine **out);
+void go2pi_destroy(go2pi_engine *e);
+
+/* I/O metadata of graph input/output `index` (0 = the bound observation / action). */
+int go2pi_num_io(const go2pi_engine *e, int32_t *n_inputs, int32_t *n_outputs);
+int go2pi_io_name(const go2pi_engine *e, int32_t is_output, int32_t index, char *buf, size_t cap);
+/* Writes up to `cap` dims; *rank receives the true rank. Symbolic dims read as -1. */
+int go2pi_io_shape(const go2pi_engine *e, int32_t is_output, int32_t index, int64_t *dims, int32_t cap,
+                   int32_t *rank);
+/* Per-robot feature counts of the bound observation / action (shape[1]). */
+int go2pi_io_dims(const go2pi_engine *e, int64_t *in_dim, int64_t *out_dim);
+
+/* Synchronous host path: obs [batch][in_dim] -> act [batch][out_dim], host memory
+   (the act() contract: reads obs at call time, overwrites act in place). */
+int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch);
+
+/* Asynchronous device path: obs/act are device pointers on e's device; enqueued on
+   `hip_stream` (a hipStream_t; NULL = the HIP null stream, as in HIP). No host sync.
+   The caller must use the same HIP runtime instance as this library (e.g. load
+   PyTorch's libamdhip64 first when sharing torch streams/tensors). */
+int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int64_t batch, void *hip_stream);
+
+/* Recurrent policies carry one hidden row per robot (engine-resident, HBM).
+   Run `steps` ticks back to back with the hidden rows kept on-chip between ticks:
+   obs_dev [steps][batch][in_dim] -> act_dev [steps][batch][out_dim]. For a
+   feed-forward policy this is `steps` independent batched calls. */
+int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int64_t steps,
+                              int64_t batch, void *hip_stream);
+
+/* Zero the hidden state of robots whose mask byte is non-zero (mask NULL = all). */
+int go2pi_reset_hidden(go2pi_engine *e, const uint8_t *mask, int64_t batch);
+/* Copy hidden state rows [0,batch) to/from host (hidden_dim floats per robot). */
+int go2pi_get_hidden(go2pi_engine *e, float *h, int64_t batch);
+int go2pi_set_hidden(go2pi_engine *e, const float *h, int64_t batch);
+int go2pi_hidden_dim(const go2pi_engine *e, int64_t *hidden_dim);
+
+/* Wait for all work queued on the engine's own stream. */
+int go2pi_sync(go2pi_engine *e);
+
+/* Algorithmic cost per robot-step (for roofline accounting in bench.py). */
+typedef struct go2pi_cost {
+  double flops_per_row;    /* 2*MAC of every contraction (+ nothing for activations) */
+  double weight_bytes;     /* fp32 parameter bytes (unpadded) */
+  double io_bytes_per_row; /* obs + action (+ 2x hidden for recurrent) bytes */
+  int32_t n_layers;
+  int32_t has_gru;
+} go2pi_cost;
+int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
+
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char *go2pi_last_error(void);
+
+/* Library version string. */
+const char *go2pi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GO2PI_H_ */

@@ -1,0 +1,148 @@
+"""ORACLE — test infrastructure only (tests/, smoke(), bench.py cpu_baseline).
+
+ctypes front-end for oracle/mlp_ref.c plus a layer-list extraction from the
+oracle's own decoded graph (oracle/onnx_ref.py). Parity status: parity
+unpinned — see oracle/onnx_ref.py.
+
+`mlp_layers(graph)` recognises the reference graph pattern
+(`onnx_inference/data/model.onnx`: Gemm(transB=1) -> Elu -> ... -> Gemm) and
+the MatMul+Add / Relu / Tanh / Sigmoid / LeakyRelu variants, independently of
+the product's C++ pattern matcher.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from . import onnx_ref
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libmlpref.so")
+_lib = None
+
+ACT = {"none": 0, "Elu": 1, "Relu": 2, "Tanh": 3, "Sigmoid": 4, "LeakyRelu": 5}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        L.mlpref_create.restype = P
+        L.mlpref_create.argtypes = [ctypes.c_int, P, P, P, P, P, P]
+        L.mlpref_run_f32.argtypes = [P, P, P, ctypes.c_long, ctypes.c_int]
+        L.mlpref_run_f64.argtypes = [P, P, P, ctypes.c_long, ctypes.c_int]
+        L.mlpref_destroy.argtypes = [P]
+        L.gruref_step_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, P, P,
+                                      ctypes.c_long, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def mlp_layers(g: onnx_ref.Graph):
+    """Return [(W[N,K] f32, b[N] f32, act_name, alpha)] for a Linear/act chain."""
+    layers = []
+    cur = g.inputs[0][0]
+    producers = {}
+    for nd in g.nodes:
+        for i in nd.inputs:
+            producers.setdefault(i, []).append(nd)
+    consumed = set()
+    while True:
+        nds = [n for n in producers.get(cur, []) if id(n) not in consumed]
+        if not nds:
+            break
+        nd = nds[0]
+        consumed.add(id(nd))
+        if nd.op_type == "Gemm":
+            W = g.inits[nd.inputs[1]].astype(np.float32)
+            if not nd.attrs.get("transB", 0):
+                W = W.T
+            W = W * np.float32(nd.attrs.get("alpha", 1.0))
+            b = g.inits[nd.inputs[2]].astype(np.float32) * np.float32(nd.attrs.get("beta", 1.0)) \
+                if len(nd.inputs) > 2 else np.zeros(W.shape[0], np.float32)
+            layers.append([np.ascontiguousarray(W), np.ascontiguousarray(b), "none", 0.0])
+        elif nd.op_type == "MatMul":
+            W = g.inits[nd.inputs[1]].astype(np.float32).T
+            layers.append([np.ascontiguousarray(W), np.zeros(W.shape[0], np.float32), "none", 0.0])
+        elif nd.op_type == "Add":
+            other = nd.inputs[1] if nd.inputs[0] == cur else nd.inputs[0]
+            layers[-1][1] = layers[-1][1] + g.inits[other].astype(np.float32)
+        elif nd.op_type in ("Elu", "Relu", "Tanh", "Sigmoid", "LeakyRelu"):
+            default = {"Elu": 1.0, "LeakyRelu": 0.01}.get(nd.op_type, 0.0)
+            layers[-1][2] = nd.op_type
+            layers[-1][3] = float(nd.attrs.get("alpha", default))
+        else:
+            raise NotImplementedError(nd.op_type)
+        cur = nd.outputs[0]
+    return [tuple(l) for l in layers]
+
+
+class MlpRef:
+    """fp32 / fp64 CPU restatement of the MLP policy forward."""
+
+    def __init__(self, layers):
+        self.layers = layers
+        L = lib()
+        nl = len(layers)
+        self._W = [np.ascontiguousarray(l[0], np.float32) for l in layers]
+        self._b = [np.ascontiguousarray(l[1], np.float32) for l in layers]
+        K = (ctypes.c_int * nl)(*[w.shape[1] for w in self._W])
+        N = (ctypes.c_int * nl)(*[w.shape[0] for w in self._W])
+        Wp = (ctypes.c_void_p * nl)(*[w.ctypes.data for w in self._W])
+        bp = (ctypes.c_void_p * nl)(*[b.ctypes.data for b in self._b])
+        act = (ctypes.c_int * nl)(*[ACT[l[2]] for l in layers])
+        al = (ctypes.c_float * nl)(*[l[3] for l in layers])
+        self.in_dim = self._W[0].shape[1]
+        self.out_dim = self._W[-1].shape[0]
+        self._h = L.mlpref_create(nl, K, N, Wp, bp, act, al)
+        if not self._h:
+            raise RuntimeError("mlpref_create failed")
+
+    @classmethod
+    def from_onnx(cls, path):
+        return cls(mlp_layers(onnx_ref.load(path)))
+
+    def f32(self, x, nthreads=0):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, self.in_dim)
+        y = np.empty((x.shape[0], self.out_dim), np.float32)
+        lib().mlpref_run_f32(self._h, x.ctypes.data, y.ctypes.data, x.shape[0], nthreads)
+        return y
+
+    def f64(self, x, nthreads=0):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, self.in_dim)
+        y = np.empty((x.shape[0], self.out_dim), np.float64)
+        lib().mlpref_run_f64(self._h, x.ctypes.data, y.ctypes.data, x.shape[0], nthreads)
+        return y
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().mlpref_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def gru_step_f64(W, R, Wb, Rb, x, h, lbr=1, nthreads=0):
+    """One ONNX GRU step in fp64. W [3H,I], R [3H,H], Wb/Rb [3H], x [B,I] f32,
+    h [B,H] f64 (updated copy returned)."""
+    W = np.ascontiguousarray(W, np.float32)
+    R = np.ascontiguousarray(R, np.float32)
+    Wb = np.ascontiguousarray(Wb, np.float32)
+    Rb = np.ascontiguousarray(Rb, np.float32)
+    x = np.ascontiguousarray(x, np.float32)
+    h = np.array(h, np.float64, copy=True, order="C")
+    I, H = W.shape[1], R.shape[1]
+    lib().gruref_step_f64(I, H, W.ctypes.data, R.ctypes.data, Wb.ctypes.data, Rb.ctypes.data, int(lbr),
+                          x.ctypes.data, h.ctypes.data, x.shape[0], nthreads)
+    return h
