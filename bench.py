@@ -144,8 +144,15 @@ def main():
     act = torch.empty((batch, eng.out_dim), device=dev)
     stream = torch.cuda.Stream(dev)  # the stream every timed launch goes to
 
+    launch = eng.device_launcher(obs.data_ptr(), act.data_ptr(), batch, stream.cuda_stream)
     for _ in range(args.warmup):
-        eng.run_torch(obs, out=act, stream=stream)
+        launch()
+    torch.cuda.synchronize(dev)
+    # host enqueue cost per launch (must stay below the kernel time for the GPU to stay fed)
+    h0 = time.perf_counter()
+    for _ in range(args.steps):
+        launch()
+    host_us = (time.perf_counter() - h0) / args.steps * 1e6
     torch.cuda.synchronize(dev)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -155,7 +162,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        eng.run_torch(obs, out=act, stream=stream)
+        launch()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -195,6 +202,7 @@ def main():
         "config": {"workload": args.workload, "description": cfg_desc, "robots_per_gpu": batch,
                    "global_batch": batch * world, "parallelism": f"fleet shards x{world} (no data-path collective)"},
         "kernel_us": round(kernel_ms * 1e3, 3),
+        "host_enqueue_us": round(host_us, 3),
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4),
                      "traffic": traffic,

@@ -49,6 +49,7 @@ struct ApiError : std::runtime_error {
 };
 
 inline int ceil16(int x) { return (x + 15) & ~15; }
+inline int ceil64(int x) { return (x + 63) & ~63; }
 
 }  // namespace
 
@@ -71,6 +72,7 @@ struct go2pi_engine {
   hipGraphExec_t graphs[GO2PI_SMALL_MAXB + 1] = {};
   hipGraph_t graph_defs[GO2PI_SMALL_MAXB + 1] = {};
   go2pi_cost cost{};
+  int64_t n_stamps = 0;
 
   ~go2pi_engine() {
     (void)hipSetDevice(device);
@@ -140,9 +142,12 @@ struct go2pi_engine {
 
 namespace {
 
-void pack_dense(const go2pi::Dense &d, std::vector<float> &w, std::vector<float> &b, int &K_pad, int &N_pad) {
-  K_pad = ceil16(d.K);
-  N_pad = ceil16(d.N);
+// K is padded to a multiple of 64 (4 chunks: the kernel's unroll); a hidden layer's
+// N to its consumer's K_pad (64), the final layer's N to 16 (one MFMA tile).
+void pack_dense(const go2pi::Dense &d, bool last, std::vector<float> &w, std::vector<float> &b, int &K_pad,
+                int &N_pad) {
+  K_pad = ceil64(d.K);
+  N_pad = last ? ceil16(d.N) : ceil64(d.N);
   const int T = N_pad / 16, C = K_pad / 16;
   w.assign((size_t)T * C * 64 * 4, 0.f);
   for (int t = 0; t < T; ++t)
@@ -214,7 +219,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   hip_check(hipSetDevice(e.device), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking), "hipStreamCreate");
 
-  e.waves = e.opts.waves == 4 ? 4 : 8;
+  // 16 waves per 16-robot workgroup (4 per SIMD) measured fastest (kernels.hip GO2PI_PF note)
+  e.waves = (e.opts.waves == 4 || e.opts.waves == 8) ? e.opts.waves : 16;
   e.small_batch = e.opts.small_batch == 0 ? GO2PI_SMALL_MAXB : std::min<int>(e.opts.small_batch, GO2PI_SMALL_MAXB);
 
   go2pi::DevProgram &p = e.prog;
@@ -227,7 +233,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   for (int l = 0; l < p.nl; ++l) {
     std::vector<float> w, b;
     int kp, np;
-    pack_dense(m.layers[l], w, b, kp, np);
+    pack_dense(m.layers[l], l == p.nl - 1, w, b, kp, np);
     auto &L = p.L[l];
     L.w = e.upload(w);
     L.bias = e.upload(b);
@@ -313,6 +319,11 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
             "hipHostMalloc");
   hip_check(hipHostGetDevicePointer((void **)&e.m_obs, e.h_obs, 0), "hipHostGetDevicePointer");
   hip_check(hipHostGetDevicePointer((void **)&e.m_act, e.h_act, 0), "hipHostGetDevicePointer");
+  if (std::getenv("GO2PI_DIAG_STAMPS")) {  // diagnostics: per-workgroup clock stamps
+    e.n_stamps = GO2PI_STAMPS_PER_WG * ((e.opts.max_batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
+    p.stamps = e.dalloc<unsigned long long>(e.n_stamps);
+    hip_check(hipMemset(p.stamps, 0, e.n_stamps * sizeof(unsigned long long)), "hipMemset");
+  }
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
 
   e.cost.flops_per_row = flops;
@@ -584,6 +595,19 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *c) {
     if (!c) throw ApiError("null cost", GO2PI_E_INVALID);
     *c = e->cost;
     return GO2PI_OK;
+  });
+}
+
+int go2pi_diag_stamps(go2pi_engine *e, uint64_t *out, int64_t n) {
+  return guarded([&] {
+    check_engine(e);
+    if (!e->prog.stamps) throw ApiError("stamps disabled (set GO2PI_DIAG_STAMPS before create)", GO2PI_E_INVALID);
+    if (!out || n < 0) throw ApiError("bad stamps buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const int64_t k = std::min(n, e->n_stamps);
+    hip_check(hipMemcpy(out, e->prog.stamps, k * sizeof(uint64_t), hipMemcpyDeviceToHost), "hipMemcpy");
+    return (int)k;
   });
 }
 

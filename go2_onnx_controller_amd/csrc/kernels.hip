@@ -27,19 +27,54 @@
 // unsharded runs are bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "program.hpp"
 
 namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Weight chunks kept in flight ahead of the MFMAs of each wave. Measured on
+// MI355X (tools/clock_probe.py, cycles per 16-robot workgroup, 48->512^3->12):
+// NW=16: PF0 112K, PF1 123K, PF2 122K, PF3 128K; NW=8: PF0 115K, PF3 144K.
+// Latency is covered by 4 waves per SIMD (TLP); deeper in-wave prefetch piles
+// up outstanding loads whose issue stalls block the MFMAs queued behind them.
+#if defined(GO2PI_DIAG_PF1)
+#define GO2PI_PF 1
+#elif defined(GO2PI_DIAG_PF2)
+#define GO2PI_PF 2
+#elif defined(GO2PI_DIAG_PF3)
+#define GO2PI_PF 3
+#else
+#define GO2PI_PF 0
+#endif
+
+// Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
+//   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
+//   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+#ifdef GO2PI_DIAG_NOMFMA
+  c.x = fmaf(a, b, c.x);
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#endif
+}
+
+// exp(x) - 1 for x <= 0 on the hardware exp2 (v_exp_f32, ~1 ulp): the literal
+// ONNX Elu formula alpha * (exp(x) - 1). Absolute error <= ~1.2e-7 (one ulp of
+// 1.0), far inside the 1e-5 contract, at ~4 VALU ops instead of libm's expm1f.
+__device__ __forceinline__ float expm1_neg(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.4426950408889634f) - 1.f;
 }
 
 __device__ __forceinline__ float act_fn(int act, float alpha, float x) {
+#ifdef GO2PI_DIAG_NOEPI
+  return x;
+#endif
   switch (act) {
-    case 1: return x > 0.f ? x : alpha * expm1f(x);            // Elu (ONNX opset 6)
+    case 1: return x > 0.f ? x : alpha * expm1_neg(x);         // Elu (ONNX opset 6)
     case 2: return x > 0.f ? x : 0.f;                          // Relu
     case 3: return tanhf(x);                                   // Tanh
     case 4: return 1.f / (1.f + expf(-x));                     // Sigmoid
@@ -67,6 +102,39 @@ __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
 // Tiles beyond T are clamped (their loads duplicate tile T-1, results unused),
 // keeping the unrolled load stream free of per-element branches.
 template <int TPW>
+__device__ __forceinline__ void mma_chunk(const float4 &a, const float4 (&b)[TPW], f32x4 (&acc)[TPW]) {
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.x, b[i].x, acc[i]);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.y, b[i].y, acc[i]);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.z, b[i].z, acc[i]);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.w, b[i].w, acc[i]);
+}
+
+template <int TPW>
+__device__ __forceinline__ void load_chunk(const float4 *const (&wp)[TPW], int c, float4 (&b)[TPW]) {
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+#ifdef GO2PI_DIAG_NOLOAD
+    const float v = __int_as_float(0x3c000000 ^ ((c * 7 + i) & 0xff));
+    b[i] = make_float4(v, v, v, v);
+#elif defined(GO2PI_DIAG_NT)
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(&wp[i][c * 64]));
+    b[i] = make_float4(v.x, v.y, v.z, v.w);
+#else
+    b[i] = wp[i][c * 64];
+#endif
+  }
+}
+
+// Chunk range [c0, c1) with (c1 - c0) % 4 == 0 (K is padded to 64 = 4 chunks).
+// Weights stream through a 4-deep register ring: the loads of chunk c+3 are in
+// flight while chunk c is multiplied (3 x TPW KiB per wave outstanding), which
+// is what the L2 -> CU path needs to approach the MFMA rate at 16 robots per CU
+// (8 FLOP per weight byte). Loads past c1 are clamped to c1-1 (valid, unused).
+template <int TPW>
 __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, const float4 *__restrict__ W,
                                           int C, int t_first, int T, int c0, int c1, int lane,
                                           f32x4 (&acc)[TPW]) {
@@ -78,45 +146,42 @@ __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, c
     wp[i] = W + (size_t)t * C * 64 + lane;
   }
   if (c0 >= c1) return;
-  float4 b[TPW];
+  const int cl = c1 - 1;
+  constexpr int D = GO2PI_PF;  // chunks of weights in flight ahead of the MFMAs
+  float4 r[4][TPW];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) b[i] = wp[i][c0 * 64];
-  for (int c = c0; c < c1; ++c) {
-    const int cn = min(c + 1, c1 - 1);
-    float4 bn[TPW];
+  for (int d = 0; d < D; ++d) load_chunk<TPW>(wp, min(c0 + d, cl), r[d]);
+  // sched_barrier(0) pins the issue order: hipcc otherwise sinks each chunk's
+  // loads next to their MFMAs and waits vmcnt(0) per chunk.
+  for (int c = c0; c < c1; c += 4) {
+    float4 a[4];
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) bn[i] = wp[i][cn * 64];
-    const float4 a = *reinterpret_cast<const float4 *>(xrow + c * 16);
+    for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.x, b[i].x, acc[i]);
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.y, b[i].y, acc[i]);
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.z, b[i].z, acc[i]);
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.w, b[i].w, acc[i]);
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) b[i] = bn[i];
+    for (int u = 0; u < 4; ++u) {
+      load_chunk<TPW>(wp, min(c + u + D, cl), r[(u + D) & 3]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_chunk<TPW>(a[u], r[u], acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
+// The bias is fetched before the contraction and added in the epilogue, so its
+// load latency hides behind the MFMA loop instead of delaying the first MFMA.
 template <int TPW>
-__device__ __forceinline__ void init_bias(f32x4 (&acc)[TPW], const float *__restrict__ bias, int t_first, int T,
+__device__ __forceinline__ void load_bias(float (&bv)[TPW], const float *__restrict__ bias, int t_first, int T,
                                           int lane) {
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int t = min(t_first + i, T - 1);
-    const float bv = bias[t * 16 + (lane & 15)];
-    acc[i] = f32x4{bv, bv, bv, bv};
-  }
+  for (int i = 0; i < TPW; ++i) bv[i] = bias[min(t_first + i, T - 1) * 16 + (lane & 15)];
 }
 
-// Epilogue of a hidden layer: activation, write the 16 x 16 tile to LDS.
-// Epilogue of the final layer: activation + post, write valid rows/cols to HBM.
+// Epilogue of a hidden layer: bias + activation, write the 16 x 16 tile to LDS.
+// Epilogue of the final layer: bias + activation + post, write valid rows/cols to HBM.
 template <int TPW>
-__device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW], int t_first,
-                                            int T, int lane, bool last, float *Y, int ys, float *out, int row0,
-                                            int B) {
+__device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW],
+                                            const float (&bv)[TPW], int t_first, int T, int lane, bool last, float *Y,
+                                            int ys, float *out, int row0, int B) {
   const int col = lane & 15, r0 = (lane >> 4) << 2;
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -125,12 +190,12 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
     const int n = t * 16 + col;
     if (!last) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_fn(L.act, L.alpha, acc[i][r]);
+      for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_fn(L.act, L.alpha, acc[i][r] + bv[i]);
     } else if (n < L.N) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + r0 + r;
-        if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_fn(L.act, L.alpha, acc[i][r]));
+        if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_fn(L.act, L.alpha, acc[i][r] + bv[i]));
       }
     }
   }
@@ -141,9 +206,12 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
                                             int t_first, int T, int C, int lane, bool last, float *out, int row0,
                                             int B) {
   f32x4 acc[TPW];
-  init_bias<TPW>(acc, L.bias, t_first, T, lane);
+  float bv[TPW];
+  load_bias<TPW>(bv, L.bias, t_first, T, lane);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t_first, T, 0, C, lane, acc);
-  dense_store<TPW>(P, L, acc, t_first, T, lane, last, Y, xs, out, row0, B);
+  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, row0, B);
 }
 
 // One dense layer for the whole workgroup (NW waves). Contains barriers only in
@@ -155,13 +223,16 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
     // tiles split over waves, full K per wave
+    // largest tile group per pass: bounded so the ring + accumulators fit the
+    // VGPR budget of NW waves per CU (512 / (NW/4) registers per lane)
+    constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
     const int tpw = (T + NW - 1) / NW;
     int t = wave * tpw;
     const int t_end = min(t + tpw, T);
-    for (; t + 8 <= t_end; t += 8) dense_group<8>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B);
+    for (; t + G <= t_end; t += G) dense_group<G>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B);
     const int rem = t_end - t;
-    if (rem > 4) dense_group<8>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
-    else if (rem > 2) dense_group<4>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    if (G > 4 && rem > 4) dense_group<G>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    else if (G > 2 && rem > 2) dense_group<(G > 4 ? 4 : G)>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
     else if (rem == 2) dense_group<2>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
     else if (rem == 1) dense_group<1>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
   } else {
@@ -169,17 +240,19 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
     const int ks = NW / T;
     const int t = wave % T, s = wave / T;
     f32x4 acc[1];
-    if (s == 0) init_bias<1>(acc, L.bias, t, T, lane);
-    else acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bv[1];
+    load_bias<1>(bv, L.bias, t, T, lane);
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s < ks) {
-      const int c0 = (s * C) / ks, c1 = ((s + 1) * C) / ks;
+      const int C4 = C >> 2;  // split on 4-chunk boundaries (dense_acc unrolls by 4)
+      const int c0 = 4 * ((s * C4) / ks), c1 = 4 * (((s + 1) * C4) / ks);
       dense_acc<1>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t, T, c0, c1, lane, acc);
       if (s > 0) scratch[wave * 64 + lane] = acc[0];
     }
     __syncthreads();
     if (s == 0) {
       for (int s2 = 1; s2 < ks; ++s2) acc[0] += scratch[(t + s2 * T) * 64 + lane];
-      dense_store<1>(P, L, acc, t, T, lane, last, Y, xs, out, row0, B);
+      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, row0, B);
     }
   }
 }
@@ -282,8 +355,10 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
   const int tpw = (Ht + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, Ht);
-  for (; t + 4 <= t_end; t += 4) gru_group<4>(G, X, Hs, Y, xs, t, lane);
-  for (; t + 2 <= t_end; t += 2) gru_group<2>(G, X, Hs, Y, xs, t, lane);
+  constexpr int GM = NW >= 16 ? 1 : (NW >= 8 ? 2 : 4);  // VGPR budget per wave count
+  for (; t + GM <= t_end; t += GM) gru_group<GM>(G, X, Hs, Y, xs, t, lane);
+  if (GM > 2)
+    for (; t + 2 <= t_end; t += 2) gru_group<2>(G, X, Hs, Y, xs, t, lane);
   for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
 }
 
@@ -303,23 +378,52 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
   const int H = P.gru.H;
-
-  if (P.has_gru) {
-    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-      const int r = e / H, k = e - r * H, row = row0 + r;
-      bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
-    }
+#ifdef GO2PI_DIAG_CLOCK
+  if (tid == 0 && P.stamps) {
+    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();
+    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 1] = __builtin_amdgcn_s_memrealtime();
   }
-  for (int step = 0; step < steps; ++step) {
+#endif
+
+  auto stage_obs = [&](int step) {
     const float *ob = obs + (size_t)step * B * P.in_dim;
-    float *ac = act + (size_t)step * B * P.out_dim;
     for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
       const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
       float v = 0.f;
       if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
       bufA[r * S + k] = v;
     }
+  };
+  // Step 0's observation loads go out first; their HBM latency overlaps the
+  // zero fill. Padded activation columns are read (against zero weights) by the
+  // next layer, so they must hold finite values: clear everything the
+  // observation does not cover, once.
+  stage_obs(0);
+  {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int tail4 = (S - P.in_pad) >> 2;
+    for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
+      const int r = e / tail4;
+      reinterpret_cast<float4 *>(bufA + r * S + P.in_pad)[e - r * tail4] = z;
+    }
+    float4 *l4 = reinterpret_cast<float4 *>(bufB);
+    const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
+    for (int e = tid; e < n4; e += NT) l4[e] = z;
+  }
+  if (P.has_gru) {
+    __syncthreads();  // bufH zero fill above before the hidden rows land
+    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+      const int r = e / H, k = e - r * H, row = row0 + r;
+      bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
+    }
+  }
+  for (int step = 0; step < steps; ++step) {
+    float *ac = act + (size_t)step * B * P.out_dim;
+    if (step > 0) stage_obs(step);
     __syncthreads();
+#ifdef GO2PI_DIAG_CLOCK
+    if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
+#endif
     float *X = bufA, *Y = bufB;
     if (P.has_gru) {
       gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
@@ -337,6 +441,10 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
       const bool last = l == P.nl - 1;
       dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, row0, B);
       __syncthreads();
+#ifdef GO2PI_DIAG_CLOCK
+      if (tid == 0 && P.stamps && step == 0 && l < 10)
+        P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
+#endif
       float *t = X;
       X = Y;
       Y = t;
@@ -348,6 +456,12 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
       if (row < B) hidden[(size_t)row * H + k] = bufH[r * S + k];
     }
   }
+#ifdef GO2PI_DIAG_CLOCK
+  if (tid == 0 && P.stamps) {
+    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 2] = __builtin_amdgcn_s_memtime();
+    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -433,15 +547,20 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
   return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
 }
 
+template <int NW>
+static hipError_t set_fused_lds(int bytes) {
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 int configure_kernels(const DevProgram &p, int waves) {
   hipError_t e = hipSuccess;
   const int bytes = (int)fused_lds_bytes(p, waves);
-  if (waves == 8)
-    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<8>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  else
-    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<4>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  switch (waves) {
+    case 4: e = set_fused_lds<4>(bytes); break;
+    case 16: e = set_fused_lds<16>(bytes); break;
+    default: e = set_fused_lds<8>(bytes); break;
+  }
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
   for (int l = 0; l < p.nl; ++l) gmax = std::max(gmax, (int)gemv_lds_bytes(p, l));
@@ -456,10 +575,17 @@ int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float 
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_lds_bytes(p, waves);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (waves == 8)
-    hipLaunchKernelGGL(policy_fused_kernel<8>, grid, dim3(512), lds, s, p, obs, act, hidden, batch, steps);
-  else
-    hipLaunchKernelGGL(policy_fused_kernel<4>, grid, dim3(256), lds, s, p, obs, act, hidden, batch, steps);
+  switch (waves) {
+    case 4:
+      hipLaunchKernelGGL(policy_fused_kernel<4>, grid, dim3(256), lds, s, p, obs, act, hidden, batch, steps);
+      break;
+    case 16:
+      hipLaunchKernelGGL(policy_fused_kernel<16>, grid, dim3(1024), lds, s, p, obs, act, hidden, batch, steps);
+      break;
+    default:
+      hipLaunchKernelGGL(policy_fused_kernel<8>, grid, dim3(512), lds, s, p, obs, act, hidden, batch, steps);
+      break;
+  }
   return (int)hipGetLastError();
 }
 

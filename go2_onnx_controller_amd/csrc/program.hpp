@@ -17,6 +17,7 @@
 #define GO2PI_MAX_LAYERS 8
 #define GO2PI_TILE_ROWS 16      // robots per workgroup tile in the batched kernel
 #define GO2PI_SMALL_MAXB 8      // max rows of the GEMV chain
+#define GO2PI_STAMPS_PER_WG 16  // diagnostics: {start, end} x {memtime, realtime} + 12 phase memtimes
 
 namespace go2pi {
 
@@ -50,6 +51,7 @@ struct DevProgram {
   int post_tanh;
   float clip_lo, clip_hi, scale;
   DevGru gru;
+  unsigned long long *stamps;  // diagnostics only (GO2PI_DIAG_CLOCK builds): 4 per workgroup
   DevLayer L[GO2PI_MAX_LAYERS];
 };
 

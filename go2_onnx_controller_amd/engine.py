@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libgo2pi.so")
+LIB_PATH = os.environ.get("GO2PI_LIB") or os.path.join(LIB_DIR, "libgo2pi.so")  # override: diagnostics only
 ACTOR_LIB_PATH = os.path.join(LIB_DIR, "libonnx_actor.so")
 
 # every symbol include/go2pi.h declares (tests check the .so exports them all)
@@ -21,7 +21,8 @@ EXPORTS = [
     "go2pi_default_opts", "go2pi_create", "go2pi_create_from_memory", "go2pi_destroy", "go2pi_num_io",
     "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
     "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
-    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_last_error", "go2pi_version",
+    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_diag_stamps", "go2pi_last_error",
+    "go2pi_version",
 ]
 
 GO2PI_OK = 0
@@ -98,6 +99,7 @@ def lib():
             "go2pi_hidden_dim": (ctypes.c_int, [P, P]),
             "go2pi_sync": (ctypes.c_int, [P]),
             "go2pi_get_cost": (ctypes.c_int, [P, P]),
+            "go2pi_diag_stamps": (ctypes.c_int, [P, P, I64]),
             "go2pi_last_error": (ctypes.c_char_p, []),
             "go2pi_version": (ctypes.c_char_p, []),
         }
@@ -200,6 +202,19 @@ class Engine:
     def run_device(self, obs_ptr, act_ptr, batch, stream=None):
         _check(lib().go2pi_run_device(self._h, obs_ptr, act_ptr, int(batch), stream))
 
+    def device_launcher(self, obs_ptr, act_ptr, batch, stream=None):
+        """Pre-bound zero-argument launcher for tight host loops: the ctypes
+        arguments are converted once, so the per-call host cost is the C ABI's."""
+        fn = lib().go2pi_run_device
+        args = (self._h, ctypes.c_void_p(obs_ptr), ctypes.c_void_p(act_ptr), ctypes.c_int64(int(batch)),
+                ctypes.c_void_p(stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _check(rc)
+        return launch
+
     def run_sequence_device(self, obs_ptr, act_ptr, steps, batch, stream=None):
         _check(lib().go2pi_run_sequence_device(self._h, obs_ptr, act_ptr, int(steps), int(batch), stream))
 
@@ -244,6 +259,14 @@ class Engine:
 
     def sync(self):
         _check(lib().go2pi_sync(self._h))
+
+    def diag_stamps(self, n):
+        """Per-workgroup {memtime, realtime} start/end stamps (diagnostic builds only)."""
+        buf = np.zeros(n, np.uint64)
+        k = lib().go2pi_diag_stamps(self._h, buf.ctypes.data, buf.size)
+        if k < 0:
+            _check(k)
+        return buf[:k]
 
     def close(self):
         if getattr(self, "_h", None):

@@ -51,7 +51,7 @@ typedef struct go2pi_opts {
   int64_t max_batch;     /* robots per call capacity (device buffers), default 4096 */
   int32_t use_graph;     /* 1 (default): the small-batch host path replays a captured hipGraph */
   int32_t log_level;     /* OrtLoggingLevel-compatible: 0 VERBOSE … 4 FATAL, default 2 */
-  int32_t waves;         /* waves per workgroup of the batched kernel: 4 or 8 (0 = auto) */
+  int32_t waves;         /* waves per workgroup of the batched kernel: 4, 8 or 16 (0 = auto: 16) */
   int32_t small_batch;   /* host batches <= this use the GEMV chain (0 = auto: 8; -1 = never) */
   /* Optional fused prologue / epilogue (north_star: obs normalisation, action tanh/clip).
      All OFF by default so act() stays comparable to the shipped graph. */
@@ -118,6 +118,11 @@ typedef struct go2pi_cost {
   int32_t has_gru;
 } go2pi_cost;
 int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
+
+/* Diagnostics: copy up to n per-workgroup clock stamps of the last batched launch
+   ({s_memtime, s_memrealtime} at start and end, 4 per workgroup). Needs a
+   GO2PI_DIAG_CLOCK build and GO2PI_DIAG_STAMPS set at create; returns the count. */
+int go2pi_diag_stamps(go2pi_engine *e, uint64_t *out, int64_t n);
 
 /* Thread-local message of the last failing call on this thread ("" if none). */
 const char *go2pi_last_error(void);

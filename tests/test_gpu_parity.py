@@ -121,7 +121,7 @@ def test_other_activations(oracle, synth_path, name, B):
         assert abs_err(e.run(x), onnx_ref.act(g, x)) <= TOL
 
 
-@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("waves", [4, 8, 16])
 @pytest.mark.parametrize("small", [-1, 8])
 def test_kernel_variants(oracle, synth_path, waves, small):
     """Both workgroup shapes of the batched kernel and the GEMV chain on/off."""

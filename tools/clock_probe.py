@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Diagnostics: in-kernel clock and per-workgroup cycles of the batched kernel.
+
+Run with GO2PI_LIB pointing at a GO2PI_DIAG_CLOCK build and GO2PI_DIAG_STAMPS=1:
+each workgroup stamps s_memtime (shader clock) and s_memrealtime (100 MHz) at
+start and end; clock = d(memtime) / d(realtime) * 100 MHz (MI355X_MICROARCH.md,
+DVFS give-back item 6). Launches back to back for `--seconds` first so the chip
+settles at the clock it holds under this load.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--waves", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--model", default="go2_mlp_512")
+    args = ap.parse_args()
+    os.environ.setdefault("GO2PI_DIAG_STAMPS", "1")
+    import numpy as np
+    import torch
+    from go2_onnx_controller_amd import Engine, synth
+    e = Engine(synth.ensure_model(args.model), max_batch=args.batch, waves=args.waves)
+    x = torch.randn(args.batch, e.in_dim, device="cuda:0")
+    y = torch.empty(args.batch, e.out_dim, device="cuda:0")
+    s = torch.cuda.Stream()
+    t0 = time.time()
+    n = 0
+    while time.time() - t0 < args.seconds:
+        for _ in range(50):
+            e.run_torch(x, out=y, stream=s)
+        n += 50
+        s.synchronize()
+    st = e.diag_stamps(16 * ((args.batch + 15) // 16)).reshape(-1, 16).astype(np.float64)
+    nl = e.cost["n_layers"]
+    marks = [st[:, 0], st[:, 4]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
+    names = ["init"] + [f"layer{l}" for l in range(nl)] + ["tail"]
+    phases = {n: float(np.median(b - a)) for n, a, b in zip(names, marks[:-1], marks[1:])}
+    cyc = st[:, 2] - st[:, 0]
+    rt = (st[:, 3] - st[:, 1]) / 100e6
+    clk = cyc / rt
+    out = {"lib": os.path.basename(os.environ.get("GO2PI_LIB", "default")), "waves": args.waves,
+           "launches": n, "clock_ghz_median": float(np.median(clk) / 1e9),
+           "clock_ghz_min": float(clk.min() / 1e9), "wg_cycles_median": float(np.median(cyc)),
+           "wg_us_median": float(np.median(rt) * 1e6), "wg_us_max": float(rt.max() * 1e6),
+           "launch_span_us": float((st[:, 3].max() - st[:, 1].min()) / 100),
+           "phase_cycles_median": phases}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
