@@ -155,7 +155,7 @@ void pack_dense(const go2pi::Dense &d, bool last, std::vector<float> &w, std::ve
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 4; ++j) {
           const int n = 16 * t + (lane & 15), k = 16 * c + 4 * (lane >> 4) + j;
-          w[(((size_t)t * C + c) * 64 + lane) * 4 + j] = (n < d.N && k < d.K) ? d.W[(size_t)n * d.K + k] : 0.f;
+          w[(((size_t)c * T + t) * 64 + lane) * 4 + j] = (n < d.N && k < d.K) ? d.W[(size_t)n * d.K + k] : 0.f;
         }
   b.assign(N_pad, 0.f);
   std::copy(d.b.begin(), d.b.end(), b.begin());
@@ -182,7 +182,7 @@ void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
               const int k = 16 * (c - Cx) + 4 * (lane >> 4) + j;
               v = g.R[(size_t)row * H + k];
             }
-            w[((((size_t)t * Cc + c) * 3 + gate) * 64 + lane) * 4 + j] = v;
+            w[((((size_t)c * Ht + t) * 3 + gate) * 64 + lane) * 4 + j] = v;
           }
 }
 
@@ -219,8 +219,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   hip_check(hipSetDevice(e.device), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking), "hipStreamCreate");
 
-  // 16 waves per 16-robot workgroup (4 per SIMD) measured fastest (kernels.hip GO2PI_PF note)
-  e.waves = (e.opts.waves == 4 || e.opts.waves == 8) ? e.opts.waves : 16;
+  // 8 waves per 16-robot workgroup (2 per SIMD) measured fastest with the
+  // interleaved schedule (kernels.hip, dense_acc note): 104K vs 106K cycles at 16
+  e.waves = (e.opts.waves == 4 || e.opts.waves == 16) ? e.opts.waves : 8;
   e.small_batch = e.opts.small_batch == 0 ? GO2PI_SMALL_MAXB : std::min<int>(e.opts.small_batch, GO2PI_SMALL_MAXB);
 
   go2pi::DevProgram &p = e.prog;
@@ -276,6 +277,16 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.in_pad = p.L[0].K_pad;
   }
   p.lds_stride = maxw + 4;  // +16 B per row: rows start on different LDS banks
+  // Every LDS column a layer reads is written first (hidden N_pad == next K_pad,
+  // the observation stage writes [0, in_pad)), except after a GRU whose H is not
+  // a multiple of 64: then the columns [H, ceil64(H)) must be cleared once.
+  p.zero_fill = (m.has_gru && m.gru.H % 64) ? 1 : 0;
+  // head fusion: a narrow final layer (<= 2 tiles) whose predecessor runs one tile
+  // group set per wave (T >= waves) is folded into the predecessor's epilogue
+  if (p.nl >= 2 && !std::getenv("GO2PI_NO_HEAD_FUSE")) {  // env: A/B diagnostics only
+    const int t_last = p.L[p.nl - 1].N_pad / 16, t_prev = p.L[p.nl - 2].N_pad / 16;
+    if (t_last <= 2 && t_prev >= e.waves) p.head_fuse = t_last;
+  }
 
   // prologue: model-defined (Sub/Div nodes) and/or opts-defined normalisation
   std::vector<float> sub = m.pre_sub, div = m.pre_div;

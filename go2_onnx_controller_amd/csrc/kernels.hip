@@ -35,21 +35,6 @@ namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Weight chunks kept in flight ahead of the MFMAs of each wave. Measured on
-// MI355X (tools/clock_probe.py, cycles per 16-robot workgroup, 48->512^3->12):
-// NW=16: PF0 112K, PF1 123K, PF2 122K, PF3 128K; NW=8: PF0 115K, PF3 144K.
-// Latency is covered by 4 waves per SIMD (TLP); deeper in-wave prefetch piles
-// up outstanding loads whose issue stalls block the MFMAs queued behind them.
-#if defined(GO2PI_DIAG_PF1)
-#define GO2PI_PF 1
-#elif defined(GO2PI_DIAG_PF2)
-#define GO2PI_PF 2
-#elif defined(GO2PI_DIAG_PF3)
-#define GO2PI_PF 3
-#else
-#define GO2PI_PF 0
-#endif
-
 // Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
 //   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
 //   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic
@@ -98,71 +83,65 @@ __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
 
 // ---------------------------------------------------------------------------
 // Dense contraction over k-chunks [c0, c1) for TPW consecutive 16-col tiles.
-// X: LDS activations [16][xs], W: packed fragments of this layer.
-// Tiles beyond T are clamped (their loads duplicate tile T-1, results unused),
-// keeping the unrolled load stream free of per-element branches.
-template <int TPW>
-__device__ __forceinline__ void mma_chunk(const float4 &a, const float4 (&b)[TPW], f32x4 (&acc)[TPW]) {
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.x, b[i].x, acc[i]);
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.y, b[i].y, acc[i]);
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.z, b[i].z, acc[i]);
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = mfma4(a.w, b[i].w, acc[i]);
-}
+// X: LDS activations [16][xs], W: this layer's fragments (chunk-major: the
+// float4 stride between consecutive chunks of one tile is TL * 64).
 
-template <int TPW>
-__device__ __forceinline__ void load_chunk(const float4 *const (&wp)[TPW], int c, float4 (&b)[TPW]) {
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
+// one weight fragment (GO2PI_DIAG_NOLOAD: register arithmetic instead, diagnostics)
+__device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int i) {
 #ifdef GO2PI_DIAG_NOLOAD
-    const float v = __int_as_float(0x3c000000 ^ ((c * 7 + i) & 0xff));
-    b[i] = make_float4(v, v, v, v);
-#elif defined(GO2PI_DIAG_NT)
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(&wp[i][c * 64]));
-    b[i] = make_float4(v.x, v.y, v.z, v.w);
+  const float v = __int_as_float(0x3c000000 ^ ((c * 7 + i) & 0xff));
+  (void)p;
+  (void)cs;
+  return make_float4(v, v, v, v);
 #else
-    b[i] = wp[i][c * 64];
+  return p[c * cs];
 #endif
-  }
 }
 
-// Chunk range [c0, c1) with (c1 - c0) % 4 == 0 (K is padded to 64 = 4 chunks).
-// Weights stream through a 4-deep register ring: the loads of chunk c+3 are in
-// flight while chunk c is multiplied (3 x TPW KiB per wave outstanding), which
-// is what the L2 -> CU path needs to approach the MFMA rate at 16 robots per CU
-// (8 FLOP per weight byte). Loads past c1 are clamped to c1-1 (valid, unused).
+// Schedule (measured on MI355X with tools/clock_probe.py, cycles per 16-robot
+// workgroup of the 48->512^3->12 step): every tile's fragment for chunk c+1 is
+// loaded right after that tile's 4 MFMAs of chunk c, so each wave keeps exactly
+// one chunk in flight and its load issue is spread between MFMAs. Alternatives
+// measured slower: no prefetch 110K (8 waves: 113K), one chunk ahead issued as a
+// burst 123K/145K, three ahead 128K/144K, vs 104K-106K for this one; the
+// MFMA-only ablation (no weight loads) is 97K-99K. sched_barrier(0) pins the
+// order (hipcc otherwise sinks loads next to their uses). Tiles beyond T clamp
+// to T - 1 (duplicate loads, results unused); loads past c1 clamp to c1 - 1.
+// Requires (c1 - c0) % 4 == 0 (K padded to 64).
 template <int TPW>
 __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, const float4 *__restrict__ W,
-                                          int C, int t_first, int T, int c0, int c1, int lane,
+                                          int TL, int t_first, int T, int c0, int c1, int lane,
                                           f32x4 (&acc)[TPW]) {
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const float4 *wp[TPW];
+  const int cs = TL * 64;
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int t = min(t_first + i, T - 1);
-    wp[i] = W + (size_t)t * C * 64 + lane;
-  }
+  for (int i = 0; i < TPW; ++i) wp[i] = W + (size_t)min(t_first + i, T - 1) * 64 + lane;
   if (c0 >= c1) return;
   const int cl = c1 - 1;
-  constexpr int D = GO2PI_PF;  // chunks of weights in flight ahead of the MFMAs
-  float4 r[4][TPW];
+  float4 cur[TPW];
 #pragma unroll
-  for (int d = 0; d < D; ++d) load_chunk<TPW>(wp, min(c0 + d, cl), r[d]);
-  // sched_barrier(0) pins the issue order: hipcc otherwise sinks each chunk's
-  // loads next to their MFMAs and waits vmcnt(0) per chunk.
+  for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0, cs, i);
   for (int c = c0; c < c1; c += 4) {
     float4 a[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      load_chunk<TPW>(wp, min(c + u + D, cl), r[(u + D) & 3]);
-      __builtin_amdgcn_sched_barrier(0);
-      mma_chunk<TPW>(a[u], r[u], acc);
-      __builtin_amdgcn_sched_barrier(0);
+      const int cn = min(c + u + 1, cl);
+      float4 nxt[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        acc[i] = mfma4(a[u].x, cur[i].x, acc[i]);
+        acc[i] = mfma4(a[u].y, cur[i].y, acc[i]);
+        acc[i] = mfma4(a[u].z, cur[i].z, acc[i]);
+        acc[i] = mfma4(a[u].w, cur[i].w, acc[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        nxt[i] = load_frag(wp[i], cn, cs, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
     }
   }
 }
@@ -201,17 +180,106 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
   }
 }
 
+// HT > 0: "head fusion". The final, narrow layer HL (HT <= 2 output tiles, e.g.
+// the 12 actions) is accumulated inside this layer: the wave's freshly stored
+// tiles are exactly its K-chunks of HL, so it multiplies them (read back from
+// LDS by the same wave) against HL's fragments, fetched before its MFMA loop.
+// Partials are summed across waves in a fixed order by head_finish (below).
+template <int TPW, int HT>
+__device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
+                                            int t_first, int T, int C, int lane, bool last, float *out, int row0,
+                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+  constexpr int HN = HT > 0 ? HT : 1;
+  f32x4 acc[TPW];
+  float bv[TPW];
+  float4 hw[HN][TPW];
+  load_bias<TPW>(bv, L.bias, t_first, T, lane);
+  if constexpr (HT > 0) {
+    const float4 *HW = reinterpret_cast<const float4 *>(HL->w);
+    const int HTL = HL->N_pad >> 4;  // head tiles (chunk-major fragments)
+#pragma unroll
+    for (int h = 0; h < HT; ++h)
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)min(t_first + i, T - 1) * HTL + h) * 64 + lane];
+  }
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc);
+  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, row0, B);
+  if constexpr (HT > 0) {
+    // this wave's own LDS stores above are read back below (other lanes' values):
+    // keep the compiler from hoisting the reads (the LDS queue is in order per wave)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const float *yrow = Y + (lane & 15) * xs + ((lane >> 4) << 2);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (t_first + i >= T) continue;
+      const float4 a = *reinterpret_cast<const float4 *>(yrow + (t_first + i) * 16);
+#pragma unroll
+      for (int h = 0; h < HT; ++h) {
+        hacc[h] = mfma4(a.x, hw[h][i].x, hacc[h]);
+        hacc[h] = mfma4(a.y, hw[h][i].y, hacc[h]);
+        hacc[h] = mfma4(a.z, hw[h][i].z, hacc[h]);
+        hacc[h] = mfma4(a.w, hw[h][i].w, hacc[h]);
+      }
+    }
+  }
+}
+
 template <int TPW>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out, int row0,
                                             int B) {
-  f32x4 acc[TPW];
-  float bv[TPW];
-  load_bias<TPW>(bv, L.bias, t_first, T, lane);
+  f32x4 none[1];
+  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, row0, B, nullptr, none);
+}
+
+// Tiles of a wide layer split over the NW waves (full K per wave), optionally
+// with the fused head (HT > 0). Barrier-free.
+template <int NW, int HT>
+__device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
+                                            int wave, int lane, bool last, float *out, int row0, int B,
+                                            const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+  const int T = L.N_pad >> 4, C = L.K_pad >> 4;
+  // largest tile group per pass: bounded so the accumulators fit the VGPR
+  // budget of NW waves per CU (512 / (NW/4) registers per lane)
+  constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
+  const int tpw = (T + NW - 1) / NW;
+  int t = wave * tpw;
+  const int t_end = min(t + tpw, T);
+  for (; t + G <= t_end; t += G) dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B, HL, hacc);
+  const int rem = t_end - t;
+  if (G > 4 && rem > 4) dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+  else if (G > 2 && rem > 2)
+    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+  else if (rem == 2) dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+  else if (rem == 1) dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+}
+
+// Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
+// partials go to LDS scratch; head_finish sums them after the layer barrier.
+template <int NW, int HT>
+__device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevLayer &L, const DevLayer &HL,
+                                                 const float *X, float *Y, int xs, f32x4 *scratch, int wave,
+                                                 int lane, int row0, int B) {
+  f32x4 hacc[HT];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t_first, T, 0, C, lane, acc);
-  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, row0, B);
+  for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, row0, B, &HL, hacc);
+#pragma unroll
+  for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
+}
+
+template <int NW>
+__device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer &HL, const f32x4 *scratch, int wave,
+                                            int lane, float *out, int row0, int B) {
+  const int T = HL.N_pad >> 4;
+  if (wave >= T) return;
+  f32x4 acc[1] = {scratch[(wave * NW) * 64 + lane]};
+  for (int w = 1; w < NW; ++w) acc[0] += scratch[(wave * NW + w) * 64 + lane];  // fixed order: deterministic
+  float bv[1];
+  load_bias<1>(bv, HL.bias, wave, T, lane);
+  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, row0, B);
 }
 
 // One dense layer for the whole workgroup (NW waves). Contains barriers only in
@@ -222,19 +290,8 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
                                             int B) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
-    // tiles split over waves, full K per wave
-    // largest tile group per pass: bounded so the ring + accumulators fit the
-    // VGPR budget of NW waves per CU (512 / (NW/4) registers per lane)
-    constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
-    const int tpw = (T + NW - 1) / NW;
-    int t = wave * tpw;
-    const int t_end = min(t + tpw, T);
-    for (; t + G <= t_end; t += G) dense_group<G>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B);
-    const int rem = t_end - t;
-    if (G > 4 && rem > 4) dense_group<G>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
-    else if (G > 2 && rem > 2) dense_group<(G > 4 ? 4 : G)>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
-    else if (rem == 2) dense_group<2>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
-    else if (rem == 1) dense_group<1>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B);
+    f32x4 none[1];
+    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, row0, B, nullptr, none);
   } else {
     // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
     const int ks = NW / T;
@@ -246,7 +303,7 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
     if (s < ks) {
       const int C4 = C >> 2;  // split on 4-chunk boundaries (dense_acc unrolls by 4)
       const int c0 = 4 * ((s * C4) / ks), c1 = 4 * (((s + 1) * C4) / ks);
-      dense_acc<1>(X, xs, reinterpret_cast<const float4 *>(L.w), C, t, T, c0, c1, lane, acc);
+      dense_acc<1>(X, xs, reinterpret_cast<const float4 *>(L.w), T, t, T, c0, c1, lane, acc);
       if (s > 0) scratch[wave * 64 + lane] = acc[0];
     }
     __syncthreads();
@@ -277,8 +334,10 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
     r[i] = f32x4{br, br, br, br};
     nx[i] = f32x4{bx, bx, bx, bx};
     nh[i] = f32x4{bh, bh, bh, bh};
-    wp[i] = W + (size_t)(t_first + i) * Cc * 192 + lane;
+    wp[i] = W + (size_t)(t_first + i) * 192 + lane;
   }
+  const int cs = (G.H >> 4) * 192;  // chunk-major: [chunk][tile][gate][lane]
+  (void)Cc;
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
   for (int c = 0; c < Cx; ++c) {
@@ -286,9 +345,9 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
     float4 wz[GT], wr[GT], wh[GT];
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
-      wz[i] = wp[i][c * 192];
-      wr[i] = wp[i][c * 192 + 64];
-      wh[i] = wp[i][c * 192 + 128];
+      wz[i] = wp[i][c * cs];
+      wr[i] = wp[i][c * cs + 64];
+      wh[i] = wp[i][c * cs + 128];
     }
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
@@ -312,9 +371,9 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
     float4 wz[GT], wr[GT], wh[GT];
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
-      wz[i] = wp[i][(Cx + c) * 192];
-      wr[i] = wp[i][(Cx + c) * 192 + 64];
-      wh[i] = wp[i][(Cx + c) * 192 + 128];
+      wz[i] = wp[i][(Cx + c) * cs];
+      wr[i] = wp[i][(Cx + c) * cs + 64];
+      wh[i] = wp[i][(Cx + c) * cs + 128];
     }
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
@@ -399,7 +458,7 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
   // next layer, so they must hold finite values: clear everything the
   // observation does not cover, once.
   stage_obs(0);
-  {
+  if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tail4 = (S - P.in_pad) >> 2;
     for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
@@ -439,6 +498,19 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
     }
     for (int l = 0; l < P.nl; ++l) {
       const bool last = l == P.nl - 1;
+      if (P.head_fuse && l == P.nl - 2) {
+        if (P.head_fuse == 1) dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
+        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
+        __syncthreads();
+        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, row0, B);
+#ifdef GO2PI_DIAG_CLOCK
+        if (tid == 0 && P.stamps && step == 0 && l < 9) {
+          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
+          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+        break;  // scratch is next written two barriers later; bufA/bufB are free
+      }
       dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, row0, B);
       __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
@@ -494,10 +566,10 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
   float p[GO2PI_SMALL_MAXB];
 #pragma unroll
   for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
-  const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)t * C * 64 + lane;
+  const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)t * 64 + lane;  // chunk-major
   const int koff = (lane >> 4) << 2;
   for (int c = wave; c < C; c += GEMV_WAVES) {
-    const float4 w = W[c * 64];
+    const float4 w = W[(size_t)c * T * 64];
 #pragma unroll
     for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
       if (b < B) {
@@ -540,7 +612,9 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
 
 // ---------------------------------------------------------------------------
 size_t fused_lds_bytes(const DevProgram &p, int waves) {
-  return sizeof(float) * (size_t)(2 + p.has_gru) * GO2PI_TILE_ROWS * p.lds_stride + sizeof(f32x4) * 64 * waves;
+  // activation buffers + per-wave partial-sum scratch (head fusion: up to 2 tiles)
+  return sizeof(float) * (size_t)(2 + p.has_gru) * GO2PI_TILE_ROWS * p.lds_stride +
+         sizeof(f32x4) * 64 * waves * (p.head_fuse > 1 ? p.head_fuse : 1);
 }
 
 size_t gemv_lds_bytes(const DevProgram &p, int layer) {

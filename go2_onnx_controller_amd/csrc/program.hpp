@@ -3,13 +3,17 @@
 //
 // Weight layout in HBM ("fragment order", built once at load time):
 // a dense layer W[N][K] (ONNX Gemm transB=1 layout) is zero-padded to
-// N_pad = ceil16(N), K_pad = ceil16(K) and stored as
-//     packed[t][c][lane] : float4,  t < N_pad/16, c < K_pad/16, lane < 64
-//     packed[t][c][lane].j = W[16t + (lane & 15)][16c + 4(lane >> 4) + j]
-// so one wave-instruction (64 lanes x 16 B) reads 1 KiB of contiguous HBM and
-// the float4 feeds four v_mfma_f32_16x16x4_f32 as the B operand (B[k][n] =
-// W[n][k]) — see kernels.hip. The GRU gates use the same idea with three gate
-// fragments per (tile, chunk).
+// N_pad (64 for hidden layers, 16 for the final one), K_pad = ceil64(K) and
+// stored chunk-major:
+//     packed[c][t][lane] : float4,  c < K_pad/16, t < N_pad/16, lane < 64
+//     packed[c][t][lane].j = W[16t + (lane & 15)][16c + 4(lane >> 4) + j]
+// so one wave-instruction (64 lanes x 16 B) reads 1 KiB of contiguous memory
+// and the float4 feeds four v_mfma_f32_16x16x4_f32 as the B operand (B[k][n] =
+// W[n][k]) — see kernels.hip. Chunk-major order keeps the slab that every CU
+// of an XCD reads at the same moment (chunk c of all tiles) contiguous, so it
+// spreads over all L2 channels instead of striding one (tile-major measured
+// slower). The GRU gates use the same idea with three gate fragments per
+// (chunk, tile): packed[c][t][gate][lane].
 #pragma once
 
 #include <cstdint>
@@ -42,6 +46,8 @@ struct DevProgram {
   int in_dim, in_pad, out_dim;
   int lds_stride;  // floats per row of an LDS activation buffer
   int has_gru;
+  int head_fuse;   // >0: the final layer (this many 16-col tiles) is fused into the one before it
+  int zero_fill;   // 1: clear LDS activation buffers at kernel start (padded columns never written)
   // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
   const float *pre_sub;
   const float *pre_div;

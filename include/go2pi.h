@@ -51,7 +51,7 @@ typedef struct go2pi_opts {
   int64_t max_batch;     /* robots per call capacity (device buffers), default 4096 */
   int32_t use_graph;     /* 1 (default): the small-batch host path replays a captured hipGraph */
   int32_t log_level;     /* OrtLoggingLevel-compatible: 0 VERBOSE … 4 FATAL, default 2 */
-  int32_t waves;         /* waves per workgroup of the batched kernel: 4, 8 or 16 (0 = auto: 16) */
+  int32_t waves;         /* waves per workgroup of the batched kernel: 4, 8 or 16 (0 = auto: 8) */
   int32_t small_batch;   /* host batches <= this use the GEMV chain (0 = auto: 8; -1 = never) */
   /* Optional fused prologue / epilogue (north_star: obs normalisation, action tanh/clip).
      All OFF by default so act() stays comparable to the shipped graph. */

@@ -1,8 +1,8 @@
 set -o pipefail
-timeout -k 10 300 python bench.py --no-cpu --no-latency > gpurun_out/b.json 2>gpurun_out/b.err || exit 1
-python3 -c "import json;d=json.load(open('gpurun_out/b.json'));print(d['value'], d['kernel_us'], d['host_enqueue_us'], d['ms_per_step'], d['roofline']['frac'])"
-TAG=w16 bash tools/profile.sh
-python3 - <<'PY'
-import csv
-for r in csv.DictReader(open('gpurun_out/prof_w16_kt/run_kernel_stats.csv')): print(r['Name'][:60], r['Calls'], r['AverageNs'], r['MinNs'], r['MaxNs'])
-PY
+R=$(pwd)
+WAVES="8 16" bash tools/gpu_check.sh || { grep -E "FAIL|Error|error" gpurun_out/tests.log | head -20; exit 1; }
+for v in clock noload_clock; do
+for w in 8 16; do
+  GO2PI_LIB=$R/go2_onnx_controller_amd/lib/diag/libgo2pi_$v.so timeout -k 10 120 python3 tools/clock_probe.py --waves $w --seconds 0.5 2>/dev/null | python3 -c "import json,sys;d=json.load(sys.stdin);print('$v w$w',d['wg_cycles_median'],d['phase_cycles_median'])" || exit 1
+done
+done
