@@ -92,14 +92,16 @@ def latency_b1(model_path, device, iters=3000, warm=300):
     return ts[len(ts) // 2], ts[int(len(ts) * 0.99)]
 
 
-def load_pmc(kernel_substr):
-    """HBM traffic per launch from a committed rocprofv3 --pmc summary (tools/profile.sh)."""
+def load_pmc(workload, kernel_substr, waves):
+    """Memory-side bytes per launch of `kernel_substr` from the committed rocprofv3
+    --pmc summary of this workload (tools/profile.sh + tools/summarize_prof.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction x2)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        for k, v in d.get("kernels", {}).items():
-            if kernel_substr in k:
+        for k, v in d.get("workloads", {}).get(workload, {}).items():
+            if kernel_substr in k and f"<{waves}>" in k:
                 return v.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -182,7 +184,7 @@ def main():
     flops_launch = cost["flops_per_row"] * batch
     bytes_launch = cost["weight_bytes"] + cost["io_bytes_per_row"] * batch
     achieved_tf = flops_launch / (kernel_ms * 1e-3) / 1e12
-    traffic = load_pmc("policy_fused_kernel")
+    traffic = load_pmc(args.workload, "policy_fused_kernel", args.waves or 8)
     eng.close()
 
     out = {

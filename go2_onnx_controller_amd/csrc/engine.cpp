@@ -609,6 +609,64 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *c) {
   });
 }
 
+int go2pi_inspect_model(const char *path, char *buf, size_t cap) {
+  return guarded([&] {
+    if (!path || !buf || cap == 0) throw ApiError("null argument", GO2PI_E_INVALID);
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw ApiError(std::string("cannot open model file '") + path + "'", GO2PI_E_MODEL);
+    std::vector<uint8_t> bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    go2pi::Model m;
+    try {
+      m = go2pi::parse_onnx(bytes.data(), bytes.size());
+    } catch (const std::exception &ex) {
+      throw ApiError(ex.what(), GO2PI_E_MODEL);
+    }
+    auto num = [](double v) {
+      if (std::isinf(v)) return std::string(v > 0 ? "1e308" : "-1e308");
+      char t[64];
+      std::snprintf(t, sizeof t, "%.17g", v);
+      return std::string(t);
+    };
+    auto sum = [](const std::vector<float> &v) {
+      double s = 0;
+      for (float x : v) s += x;
+      return s;
+    };
+    auto io = [&](const std::vector<go2pi::IoInfo> &v) {
+      std::string s = "[";
+      for (size_t i = 0; i < v.size(); ++i) {
+        s += (i ? "," : "") + std::string("{\"name\":\"") + v[i].name + "\",\"shape\":[";
+        for (size_t d = 0; d < v[i].shape.size(); ++d) s += (d ? "," : "") + std::to_string(v[i].shape[d]);
+        s += "]}";
+      }
+      return s + "]";
+    };
+    std::string j = "{\"ir_version\":" + std::to_string(m.ir_version) + ",\"opset\":" + std::to_string(m.opset) +
+                    ",\"producer\":\"" + m.producer + "\",\"inputs\":" + io(m.inputs) + ",\"outputs\":" +
+                    io(m.outputs) + ",\"in_dim\":" + std::to_string(m.in_dim) +
+                    ",\"out_dim\":" + std::to_string(m.out_dim) + ",\"layers\":[";
+    for (size_t l = 0; l < m.layers.size(); ++l) {
+      const auto &d = m.layers[l];
+      j += (l ? "," : "") + std::string("{\"K\":") + std::to_string(d.K) + ",\"N\":" + std::to_string(d.N) +
+           ",\"act\":" + std::to_string(d.act) + ",\"alpha\":" + num(d.alpha) + ",\"w_sum\":" + num(sum(d.W)) +
+           ",\"b_sum\":" + num(sum(d.b)) + "}";
+    }
+    j += "],\"gru\":";
+    if (m.has_gru)
+      j += "{\"I\":" + std::to_string(m.gru.I) + ",\"H\":" + std::to_string(m.gru.H) + ",\"lbr\":" +
+           std::to_string(m.gru.lbr) + ",\"w_sum\":" + num(sum(m.gru.W)) + ",\"r_sum\":" + num(sum(m.gru.R)) +
+           ",\"b_sum\":" + num(sum(m.gru.Wb) + sum(m.gru.Rb)) + "}";
+    else
+      j += "null";
+    j += ",\"pre_sub\":" + std::to_string(m.pre_sub.size()) + ",\"pre_div\":" + std::to_string(m.pre_div.size()) +
+         ",\"clip\":[" + num(m.clip_lo) + "," + num(m.clip_hi) + "]}";
+    const size_t k = std::min(cap - 1, j.size());
+    std::memcpy(buf, j.data(), k);
+    buf[k] = 0;
+    return (int)j.size();
+  });
+}
+
 int go2pi_diag_stamps(go2pi_engine *e, uint64_t *out, int64_t n) {
   return guarded([&] {
     check_engine(e);

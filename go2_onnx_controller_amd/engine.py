@@ -21,8 +21,8 @@ EXPORTS = [
     "go2pi_default_opts", "go2pi_create", "go2pi_create_from_memory", "go2pi_destroy", "go2pi_num_io",
     "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
     "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
-    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_diag_stamps", "go2pi_last_error",
-    "go2pi_version",
+    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_inspect_model", "go2pi_diag_stamps",
+    "go2pi_last_error", "go2pi_version",
 ]
 
 GO2PI_OK = 0
@@ -100,6 +100,7 @@ def lib():
             "go2pi_sync": (ctypes.c_int, [P]),
             "go2pi_get_cost": (ctypes.c_int, [P, P]),
             "go2pi_diag_stamps": (ctypes.c_int, [P, P, I64]),
+            "go2pi_inspect_model": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_last_error": (ctypes.c_char_p, []),
             "go2pi_version": (ctypes.c_char_p, []),
         }
@@ -288,3 +289,17 @@ class Engine:
 
 def version():
     return lib().go2pi_version().decode()
+
+
+def inspect_model(path):
+    """The C++ loader's view of an ONNX policy (no device needed): dict."""
+    import json
+    cap = 1 << 16
+    buf = ctypes.create_string_buffer(cap)
+    n = lib().go2pi_inspect_model(os.fsencode(path), buf, cap)
+    if n < 0:
+        _check(n)
+    if n >= cap:
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().go2pi_inspect_model(os.fsencode(path), buf, n + 1)
+    return json.loads(buf.value.decode())

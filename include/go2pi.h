@@ -119,6 +119,12 @@ typedef struct go2pi_cost {
 } go2pi_cost;
 int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
 
+/* Parse and lower an ONNX policy WITHOUT touching a device (no compute): writes a
+   JSON description (I/O names and shapes, the lowered layer program with
+   per-layer weight/bias checksums) into buf. Returns the JSON length (>= 0) or an
+   error code; truncates to cap-1 bytes. For loader tests and tooling. */
+int go2pi_inspect_model(const char *onnx_path, char *buf, size_t cap);
+
 /* Diagnostics: copy up to n per-workgroup clock stamps of the last batched launch
    ({s_memtime, s_memrealtime} at start and end, 4 per workgroup). Needs a
    GO2PI_DIAG_CLOCK build and GO2PI_DIAG_STAMPS set at create; returns the count. */

@@ -220,7 +220,7 @@ int gruref_step_f64(int I, int H, const float *W, const float *R, const float *W
     double *rg = (double *)malloc(sizeof(double) * H);
     double *zg = (double *)malloc(sizeof(double) * H);
     for (int j = 0; j < H; ++j) {
-      double az = Wb[j] + Rb[j], ar = Wb[H + j] + Rb[H + j];
+      double az = (double)Wb[j] + (double)Rb[j], ar = (double)Wb[H + j] + (double)Rb[H + j];
       for (int k = 0; k < I; ++k) {
         az += (double)W[(size_t)j * I + k] * xr[k];
         ar += (double)W[(size_t)(H + j) * I + k] * xr[k];
@@ -241,7 +241,7 @@ int gruref_step_f64(int I, int H, const float *W, const float *R, const float *W
         hn[j] = tanh(ax + rg[j] * ah);
       } else {
         for (int k = 0; k < H; ++k) ah += (double)R[(size_t)(2 * H + j) * H + k] * (rg[k] * hr[k]);
-        hn[j] = tanh(ax + ah + Rb[2 * H + j]);
+        hn[j] = tanh(ax + ah + (double)Rb[2 * H + j]);
       }
     }
     for (int j = 0; j < H; ++j) hr[j] = (1. - zg[j]) * hn[j] + zg[j] * hr[j];

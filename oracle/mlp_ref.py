@@ -81,6 +81,8 @@ def mlp_layers(g: onnx_ref.Graph):
             default = {"Elu": 1.0, "LeakyRelu": 0.01}.get(nd.op_type, 0.0)
             layers[-1][2] = nd.op_type
             layers[-1][3] = float(nd.attrs.get("alpha", default))
+        elif nd.op_type in ("Sub", "Div", "Clip", "Identity", "Flatten"):
+            pass  # prologue / epilogue elementwise ops: not dense layers (onnx_ref.act evaluates them)
         else:
             raise NotImplementedError(nd.op_type)
         cur = nd.outputs[0]

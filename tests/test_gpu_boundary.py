@@ -1,0 +1,110 @@
+"""GPU: the boundary end to end — the drop-in C++ ONNXActor in the reference
+controller's call pattern, the Python mirrors, loader breadth through the
+kernels, and the sharded fleet step (2 ranks, one GPU, gloo gather)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import graphs
+from conftest import GOLDEN, ROOT, SHIPPED, abs_err, rel_err
+from test_cpu_boundary import build_controller_shape
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.mark.parametrize("mode", ["zeros", "twos"])
+def test_cpp_onnx_actor_known_answers(mode):
+    """tests/cpp/controller_shape.cpp: make_unique<ONNXActor>(path, std::array<float,98>&,
+    std::array<float,12>&), print_model_info(), act() — as controller.cpp:25,49,215."""
+    exe = build_controller_shape()
+    r = subprocess.run([exe, SHIPPED, mode], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[:5] == ["Input dimension: 98", "Output dimension: 12", "Input name: observation",
+                         "Output name: action", "check_dims: 1"]
+    act = np.array([float(v) for v in next(l for l in lines if l.startswith("Action:")).split()[1:]])
+    want = np.load(os.path.join(GOLDEN, "golden_shipped.npz"))[f"{mode}_y"][0]
+    assert rel_err(act, want) <= TOL
+
+
+def test_cpp_onnx_actor_ticks():
+    exe = build_controller_shape()
+    r = subprocess.run([exe, SHIPPED, "ticks", "500"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "best_us:" in r.stdout
+
+
+def test_python_onnx_actor_aliasing(capsys):
+    from go2_onnx_controller_amd import ONNXActor
+    from oracle import mlp_ref
+    obs = np.zeros(98, np.float32)
+    act = np.zeros(12, np.float32)
+    actor = ONNXActor(SHIPPED, obs, act)
+    actor.print_model_info()
+    assert capsys.readouterr().out.splitlines() == ["Input dimension: 98", "Output dimension: 12",
+                                                    "Input name: observation", "Output name: action"]
+    assert actor.check_dims()
+    ref = mlp_ref.MlpRef.from_onnx(SHIPPED)
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        obs[:] = rng.standard_normal(98)   # caller writes in place, like populate_buffer
+        actor.act()
+        assert abs_err(act, ref.f64(obs)[0]) <= TOL
+    assert not ONNXActor(SHIPPED, np.zeros(100, np.float32), np.zeros(12, np.float32)).check_dims()
+
+
+def test_inference_session_mirror():
+    """The reference Python driver's calls (src/python/main.py:8-27)."""
+    from go2_onnx_controller_amd import InferenceSession
+    sess = InferenceSession(SHIPPED)
+    inp, out = sess.get_inputs()[0], sess.get_outputs()[0]
+    assert (inp.name, inp.shape, out.name, out.shape) == ("observation", [1, 98], "action", [1, 12])
+    y = sess.run([out.name], {inp.name: np.ones(inp.shape, dtype=np.float32) * 2})[0]
+    want = np.load(os.path.join(GOLDEN, "golden_shipped.npz"))["twos_y"]
+    assert rel_err(y, want) <= TOL
+
+
+@pytest.mark.parametrize("kind", graphs.VARIANTS)
+@pytest.mark.parametrize("B", [1, 5, 300])
+def test_graph_variants_on_gpu(tmp_path, kind, B):
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    p = graphs.write(tmp_path, kind, seed=B)
+    g = onnx_ref.load(p)
+    x = np.random.default_rng(B).standard_normal((B, g.inputs[0][1][1])).astype(np.float32) * 2
+    want = onnx_ref.act(g, x.astype(np.float64))
+    # relu_deep's outputs reach |600|: there fp32 itself (the CPU path, evaluated in
+    # float32 by the oracle) is up to 4.9e-5 relative off fp64, so the bound is
+    # max(1e-5, 1.5 x the CPU fp32 error), relative — as in test_shipped_stress
+    tol = max(TOL, 1.5 * rel_err(onnx_ref.act(g, x, dtype=np.float32), want))
+    with Engine(p, max_batch=512) as e:
+        assert rel_err(e.run(x), want) <= tol
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_fleet_two_ranks_bitwise(tmp_path, synth_path):
+    """Two processes each run their contiguous shard on the GPU and all-gather the
+    actions (gloo); the result equals the unsharded batch bit for bit."""
+    from go2_onnx_controller_amd import Engine
+    batch, path = 4096, synth_path("go2_mlp_512")
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               FLEET_BATCH=str(batch), FLEET_MODEL=path, FLEET_OUT=str(tmp_path))
+    worker = os.path.join(ROOT, "tests", "fleet_gpu_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker], env=dict(env, RANK=str(r))) for r in range(2)]
+    assert [p.wait(timeout=300) for p in procs] == [0, 0]
+    obs = np.random.default_rng(77).standard_normal((batch, 48)).astype(np.float32)
+    with Engine(path, max_batch=batch) as e:
+        want = e.run(obs)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"rank{r}.npy"), want)
