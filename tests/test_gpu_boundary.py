@@ -79,12 +79,15 @@ def test_graph_variants_on_gpu(tmp_path, kind, B):
     g = onnx_ref.load(p)
     x = np.random.default_rng(B).standard_normal((B, g.inputs[0][1][1])).astype(np.float32) * 2
     want = onnx_ref.act(g, x.astype(np.float64))
-    # relu_deep's outputs reach |600|: there fp32 itself (the CPU path, evaluated in
-    # float32 by the oracle) is up to 4.9e-5 relative off fp64, so the bound is
-    # max(1e-5, 1.5 x the CPU fp32 error), relative — as in test_shipped_stress
-    tol = max(TOL, 1.5 * rel_err(onnx_ref.act(g, x, dtype=np.float32), want))
+    # These graphs have unnormalised N(0, 0.3^2) weights: relu_deep's activations
+    # reach |600| and small outputs arise by cancellation, where even the CPU fp32
+    # path (oracle in float32) is 4.9e-5 off element-wise. The fp32 rounding scale
+    # is the activations' magnitude, so the bound is normwise:
+    # max|y - ref| / max(1, max|ref|) <= 1e-5.
     with Engine(p, max_batch=512) as e:
-        assert rel_err(e.run(x), want) <= tol
+        y = e.run(x)
+    assert abs_err(y, want) / max(1.0, float(np.abs(want).max())) <= TOL
+    assert abs_err(onnx_ref.act(g, x, dtype=np.float32), want) / max(1.0, float(np.abs(want).max())) <= TOL
 
 
 def _free_port():
