@@ -119,6 +119,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for the barrier / max-time reduce (nccl = RCCL)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="testing only: every rank on device 0 (rehearse N>1 on a 1-GPU box with gloo)")
     args = ap.parse_args()
 
     import torch
@@ -127,9 +131,12 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
@@ -173,7 +180,7 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # avg launch duration on the launching stream
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
