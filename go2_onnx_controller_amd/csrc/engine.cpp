@@ -14,6 +14,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -73,6 +74,15 @@ struct go2pi_engine {
   hipGraph_t graph_defs[GO2PI_SMALL_MAXB + 1] = {};
   go2pi_cost cost{};
   int64_t n_stamps = 0;
+  // single-launch small-batch path (policy_latency_kernel)
+  bool latency_ok = false;
+  unsigned long long *d_gran = nullptr;  // [nl-1][gstride] {tag, value} granules
+  int gstride = 0;
+  unsigned *h_err = nullptr, *m_err = nullptr;    // host-mapped timeout word
+  unsigned *h_done = nullptr, *m_done = nullptr;  // host-mapped completion word (own cache line)
+  bool done_ok = false;                            // final layer is one tile: WG 0 signals completion
+  go2pi::DevProgram *d_prog = nullptr;             // device copy of prog (latency kernel argument)
+  unsigned epoch = 1, last_epoch = 0;
 
   ~go2pi_engine() {
     (void)hipSetDevice(device);
@@ -84,6 +94,7 @@ struct go2pi_engine {
     for (void *p : allocs) (void)hipFree(p);
     if (h_obs) (void)hipHostFree(h_obs);
     if (h_act) (void)hipHostFree(h_act);
+    if (h_err) (void)hipHostFree(h_err);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -105,9 +116,24 @@ struct go2pi_engine {
     return !model.has_gru && small_batch > 0 && batch <= small_batch;
   }
 
+  bool use_latency(int64_t batch) const { return latency_ok && batch <= GO2PI_SMALL_MAXB; }
+
   // Enqueue one forward over `batch` rows (obs/act: device-accessible pointers).
-  void enqueue(const float *obs, float *act, int64_t batch, hipStream_t s) {
-    if (use_chain(batch)) {
+  // done (single-launch path only): host-mapped word the kernel sets to the call's epoch.
+  void enqueue(const float *obs, float *act, int64_t batch, hipStream_t s, unsigned *done = nullptr) {
+    if (use_latency(batch)) {
+      const unsigned n = (unsigned)prog.nl;
+      if (epoch > 0xFFFFFFFFu - 2 * n) {  // tag space exhausted (~1e9 calls): clear granules, restart
+        hip_check(hipMemsetAsync(d_gran, 0, sizeof(unsigned long long) * (size_t)(prog.nl - 1) * gstride, s),
+                  "hipMemsetAsync");
+        epoch = 1;
+      }
+      const unsigned e0 = epoch;
+      epoch += n;
+      last_epoch = e0;
+      hip_check(go2pi::launch_latency(prog, d_prog, obs, act, (int)batch, e0, d_gran, gstride, m_err, done, s),
+                "latency launch");
+    } else if (use_chain(batch)) {
       const float *x = obs;
       int xs = prog.in_dim;
       for (int l = 0; l < prog.nl; ++l) {
@@ -330,11 +356,35 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
             "hipHostMalloc");
   hip_check(hipHostGetDevicePointer((void **)&e.m_obs, e.h_obs, 0), "hipHostGetDevicePointer");
   hip_check(hipHostGetDevicePointer((void **)&e.m_act, e.h_act, 0), "hipHostGetDevicePointer");
+
+  // single-launch small-batch path: dense programs whose layers fit the kernel's
+  // register slots (K_pad <= 1024) and whose widest layer fits one resident grid
+  {
+    int kmax = 0;
+    for (int l = 0; l < p.nl; ++l) kmax = std::max(kmax, p.L[l].K_pad);
+    e.latency_ok = !m.has_gru && kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
+                   !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
+    if (e.latency_ok) {
+      e.gstride = GO2PI_SMALL_MAXB * maxw;
+      const size_t ng = (size_t)std::max(1, p.nl - 1) * e.gstride;
+      e.d_gran = e.dalloc<unsigned long long>(ng);
+      hip_check(hipMemset(e.d_gran, 0, ng * sizeof(unsigned long long)), "hipMemset");
+      hip_check(hipHostMalloc((void **)&e.h_err, 256, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+      std::memset(e.h_err, 0, 256);
+      hip_check(hipHostGetDevicePointer((void **)&e.m_err, e.h_err, 0), "hipHostGetDevicePointer");
+      e.h_done = e.h_err + 32;  // 128 B apart: its own cache line
+      e.m_done = e.m_err + 32;
+      e.done_ok = p.L[p.nl - 1].N_pad == 16;
+    }
+  }
   if (std::getenv("GO2PI_DIAG_STAMPS")) {  // diagnostics: per-workgroup clock stamps
     e.n_stamps = GO2PI_STAMPS_PER_WG * ((e.opts.max_batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
     p.stamps = e.dalloc<unsigned long long>(e.n_stamps);
     hip_check(hipMemset(p.stamps, 0, e.n_stamps * sizeof(unsigned long long)), "hipMemset");
   }
+  // the finished program, copied to device memory for the latency kernel
+  e.d_prog = e.dalloc<go2pi::DevProgram>(1);
+  hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
 
   e.cost.flops_per_row = flops;
@@ -482,12 +532,30 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
     if (batch <= GO2PI_SMALL_MAXB) {
       // pinned host-mapped staging: kernels read obs / write act over PCIe directly
       std::memcpy(e->h_obs, obs, in_b);
-      if (e->opts.use_graph) {
-        hip_check(hipGraphLaunch(e->graph_for((int)batch), e->stream), "hipGraphLaunch");
-      } else {
+      bool synced = false;
+      if (e->use_latency(batch)) {
+        // one direct launch (per-call epoch argument); completion observed by spinning on
+        // the host-mapped done word (a stream sync costs ~10 us more on this stack)
+        e->enqueue(e->m_obs, e->m_act, batch, e->stream, e->done_ok ? e->m_done : nullptr);
+        if (e->done_ok) {
+          const unsigned want = e->last_epoch;
+          const auto t0 = std::chrono::steady_clock::now();
+          for (unsigned it = 0; __atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) != want; ++it) {
+            __builtin_ia32_pause();
+            if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+          }
+          synced = __atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) == want;
+        }
+      } else if (!e->opts.use_graph) {
         e->enqueue(e->m_obs, e->m_act, batch, e->stream);
+      } else {
+        hip_check(hipGraphLaunch(e->graph_for((int)batch), e->stream), "hipGraphLaunch");
       }
-      hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      if (e->h_err && __atomic_load_n(e->h_err, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(e->h_err, 0u, __ATOMIC_RELEASE);
+        throw HipError("batch-1 kernel hand-off timed out (workgroups not co-resident?)", GO2PI_E_DEVICE);
+      }
       std::memcpy(act, e->h_act, out_b);
     } else {
       hip_check(hipMemcpyAsync(e->d_obs, obs, in_b, hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync H2D");

@@ -553,6 +553,17 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x;
   float *part = xs + GO2PI_SMALL_MAXB * K_pad;  // [GEMV_WAVES][B][16]
+  // Weights and bias do not depend on the input: issue their loads first so
+  // their latency overlaps the input staging (wave w owns chunks w, w+8, ...).
+  constexpr int MAXS = 8;  // chunk slots per wave: K_pad <= 8 * 8 * 16 = 1024 in registers
+  const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)t * 64 + lane;  // chunk-major
+  float4 wr[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    const int c = wave + s * GEMV_WAVES;
+    wr[s] = c < C ? W[(size_t)c * T * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float bv = (wave == 0 && lane < 16) ? L.bias[t * 16 + lane] : 0.f;
   for (int e = tid; e < B * K_pad; e += GEMV_WAVES * 64) {
     const int b = e / K_pad, k = e - b * K_pad;
     float v = 0.f;
@@ -566,10 +577,8 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
   float p[GO2PI_SMALL_MAXB];
 #pragma unroll
   for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
-  const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)t * 64 + lane;  // chunk-major
   const int koff = (lane >> 4) << 2;
-  for (int c = wave; c < C; c += GEMV_WAVES) {
-    const float4 w = W[(size_t)c * T * 64];
+  auto accumulate = [&](int c, const float4 &w) {
 #pragma unroll
     for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
       if (b < B) {
@@ -580,7 +589,13 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
         p[b] = fmaf(a.w, w.w, p[b]);
       }
     }
+  };
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    const int c = wave + s * GEMV_WAVES;
+    if (c < C) accumulate(c, wr[s]);
   }
+  for (int c = wave + MAXS * GEMV_WAVES; c < C; c += GEMV_WAVES) accumulate(c, W[(size_t)c * T * 64]);
 #pragma unroll
   for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
     p[b] += __shfl_xor(p[b], 16);
@@ -595,7 +610,6 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
   if (wave == 0 && lane < 16) {
     const int n = t * 16 + lane;
     const bool last = layer == P.nl - 1;
-    const float bv = L.bias[n];
     for (int b = 0; b < B; ++b) {
       float s = 0.f;
       for (int w2 = 0; w2 < GEMV_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
@@ -608,6 +622,163 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
     }
   }
   (void)T;
+}
+
+// ---------------------------------------------------------------------------
+// policy_latency_kernel — the batch-1 act() path in ONE launch (B <= 4).
+// One workgroup per 16-output tile of the widest layer; each layer: the
+// workgroup prefetches its weight fragments into registers, gathers the layer
+// input, reduces its 16 outputs over 8 waves, and publishes them as 8-byte
+// {tag, value} granules (cdna_hip_programming.md Guideline 16 recipe R2: one
+// aligned agent-scope relaxed store per granule; the consumer's single wave
+// re-reads until every tag equals the layer's epoch — no flag, no fence, no
+// counter, correct for any workgroup->XCD placement). Tags = epoch0 + layer,
+// epoch0 advanced by the host every call, so granules of earlier calls never
+// match. Spins are bounded: on timeout the workgroup writes `err` and stops.
+constexpr int LAT_WAVES = 8;
+constexpr int LAT_MAXS = 8;  // chunk slots per wave held in registers (K_pad <= 1024)
+
+__device__ __forceinline__ bool sweep_layer(unsigned long long *gran, int n, unsigned tag, float *dst,
+                                            unsigned *err, int lane) {
+  constexpr int U = 8;  // granules per lane per batch: all loads issued before any is checked
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    for (int base = 0; base < n; base += 64 * U) {
+      unsigned long long v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)  // clamped index: no branch around the loads
+        v[u] = __hip_atomic_load(gran + min(base + u * 64 + lane, n - 1), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * 64 + lane;
+        if (i < n) {
+          ok &= (unsigned)(v[u] >> 32) == tag;
+          dst[i] = __uint_as_float((unsigned)v[u]);
+        }
+      }
+    }
+    if (__all(ok)) return true;
+    if (spins > (1u << 22)) {  // ~seconds: a producer never ran (non-resident grid) -> give up
+      if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const DevProgram *__restrict__ Pd,
+                                                                        const float *obs, float *act, int B,
+                                                                        unsigned epoch0, unsigned long long *gran,
+                                                                        int gstride, unsigned *err, unsigned *done) {
+  // the program lives in device memory (uploaded once): a ~60-byte kernarg
+  // instead of the ~700-byte DevProgram keeps the per-launch host cost down
+  const DevProgram &P = *Pd;
+  extern __shared__ float4 lds4[];
+  float *xs = reinterpret_cast<float *>(lds4);               // [B][K_pad] layer input
+  float *part = xs + GO2PI_SMALL_MAXB * P.lds_stride;        // [waves][B][16] partial sums
+  int &abort_flag = *reinterpret_cast<int *>(part + LAT_WAVES * GO2PI_SMALL_MAXB * 16);  // in the one LDS region
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) abort_flag = 0;
+  for (int l = 0; l < P.nl; ++l) {
+    const DevLayer &L = P.L[l];
+    const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
+    if (g >= T) continue;  // this workgroup owns no tile of layer l
+    const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)g * 64 + lane;
+    float4 wr[LAT_MAXS];
+#pragma unroll
+    for (int s = 0; s < LAT_MAXS; ++s) {
+      const int c = wave + s * LAT_WAVES;
+      wr[s] = c < C ? W[(size_t)c * T * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
+    if (l == 0) {
+      for (int e = tid; e < B * K_pad; e += LAT_WAVES * 64) {
+        const int b = e / K_pad, k = e - b * K_pad;
+        xs[e] = k < P.in_dim ? prologue(P, obs[(size_t)b * P.in_dim + k], k) : 0.f;
+      }
+    } else if (wave == 0) {
+      if (!sweep_layer(gran + (size_t)(l - 1) * gstride, B * K_pad, epoch0 + (unsigned)(l - 1), xs, err, lane))
+        abort_flag = 1;
+    }
+    __syncthreads();
+    if (abort_flag) return;
+    float p[GO2PI_SMALL_MAXB];
+#pragma unroll
+    for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
+    const int koff = (lane >> 4) << 2;
+#pragma unroll
+    for (int s = 0; s < LAT_MAXS; ++s) {
+      const int c = wave + s * LAT_WAVES;
+      if (c >= C) break;
+#pragma unroll
+      for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+        if (b < B) {
+          const float4 a = *reinterpret_cast<const float4 *>(xs + b * K_pad + c * 16 + koff);
+          p[b] = fmaf(a.x, wr[s].x, p[b]);
+          p[b] = fmaf(a.y, wr[s].y, p[b]);
+          p[b] = fmaf(a.z, wr[s].z, p[b]);
+          p[b] = fmaf(a.w, wr[s].w, p[b]);
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+      p[b] += __shfl_xor(p[b], 16);
+      p[b] += __shfl_xor(p[b], 32);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int b = 0; b < GO2PI_SMALL_MAXB; ++b)
+        if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
+    }
+    __syncthreads();
+    if (wave == 0 && lane < 16) {
+      const int n = g * 16 + lane;
+      const bool last = l == P.nl - 1;
+      for (int b = 0; b < B; ++b) {
+        float s = 0.f;
+        for (int w2 = 0; w2 < LAT_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
+        const float v = act_fn(L.act, L.alpha, s + bv);
+        if (last) {
+          if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
+          if (done && b == B - 1 && g == 0) {
+            // completion word for the host's spin (instead of a stream sync): every
+            // action store of this tile drained and made system-visible first
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0 && T == 1) __hip_atomic_store(done, epoch0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        } else {
+          const unsigned long long gv = ((unsigned long long)(epoch0 + (unsigned)l) << 32) | __float_as_uint(v);
+          __hip_atomic_store(gran + (size_t)l * gstride + b * L.N_pad + n, gv, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    __syncthreads();  // xs / part reused by the next layer
+  }
+}
+
+int latency_grid(const DevProgram &p) {
+  int grid = 1;
+  for (int l = 0; l < p.nl; ++l) grid = std::max(grid, p.L[l].N_pad >> 4);
+  return grid;
+}
+
+int launch_latency(const DevProgram &p, const DevProgram *p_dev, const float *obs, float *act, int batch,
+                   unsigned epoch0,
+                   unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream) {
+  if (batch <= 0) return 0;
+  if (batch > GO2PI_SMALL_MAXB) return (int)hipErrorInvalidValue;
+  const int grid = latency_grid(p);
+  const size_t lds =
+      sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + LAT_WAVES * GO2PI_SMALL_MAXB * 16 + 4);
+  hipLaunchKernelGGL(policy_latency_kernel, dim3(grid), dim3(LAT_WAVES * 64), lds,
+                     reinterpret_cast<hipStream_t>(stream), p_dev, obs, act, batch, epoch0, gran, gstride, err,
+                     done);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

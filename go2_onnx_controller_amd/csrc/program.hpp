@@ -70,5 +70,14 @@ int launch_gemv_layer(const DevProgram &p, int layer, const float *x, int x_stri
                       int batch, void *stream);
 size_t gemv_lds_bytes(const DevProgram &p, int layer);
 int configure_kernels(const DevProgram &p, int waves);
+// batch <= GO2PI_SMALL_MAXB act() in one launch; gran: [nl-1][gstride] u64 granules
+// (tag = epoch0 + layer), err: host-visible word set to 1 on a hand-off timeout,
+// done: host-visible word set to epoch0 once the action is written (final layer
+// must be a single 16-output tile; may be null).
+// p_dev: a device-memory copy of p (the kernel reads the program from it).
+int launch_latency(const DevProgram &p, const DevProgram *p_dev, const float *obs, float *act, int batch,
+                   unsigned epoch0,
+                   unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream);
+int latency_grid(const DevProgram &p);
 
 }  // namespace go2pi

@@ -123,6 +123,8 @@ MODELS = {
     "mlp_small_relu": lambda: mlp_model_bytes((20, 64, 40, 5), seed=3, act="Relu"),
     "mlp_small_tanh": lambda: mlp_model_bytes((33, 48, 7), seed=4, act="Tanh"),
     "gru_small": lambda: gru_model_bytes(I=10, H=32, head=(64, 6), seed=5),
+    # launch/sync floor probe (tools/latency_probe.py)
+    "tiny": lambda: mlp_model_bytes((4, 16, 4), seed=6),
 }
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -1,3 +1,6 @@
 set -o pipefail
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -2 gpurun_out/smoke.log
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 --dist-backend gloo --same-device > gpurun_out/b2.json 2> gpurun_out/b2.err; echo "torchrun rc=$?"; cat gpurun_out/b2.json | cut -c1-400
+timeout -k 10 600 python -m pytest tests/ -m gpu -q -x > gpurun_out/tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/tests.log; [ $rc = 0 ] || { grep -E "^E |FAILED" gpurun_out/tests.log | head; exit 1; }
+for a in "--model tiny" "" "--model shipped"; do
+  timeout -k 10 120 python3 tools/latency_probe.py $a 2>/dev/null || exit 1
+done
+timeout -k 10 120 ./build/controller_shape tests/golden/model.onnx ticks 5000 | tail -1
