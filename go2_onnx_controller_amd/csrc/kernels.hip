@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "program.hpp"
 
@@ -54,17 +55,50 @@ __device__ __forceinline__ float expm1_neg(float x) {
   return __builtin_amdgcn_exp2f(x * 1.4426950408889634f) - 1.f;
 }
 
-__device__ __forceinline__ float act_fn(int act, float alpha, float x) {
+// sigmoid on v_exp_f32 + v_rcp_f32 (each ~1 ulp): ~2e-7 relative, no IEEE
+// division sequence. exp2 of a large positive argument gives +inf -> rcp -> 0.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
+// Activation with the kind known at compile time: epilogues dispatch ONCE per
+// tile group (a runtime switch per element made hipcc emit every activation's
+// code, an IEEE divide and a vmcnt(0) wait for each of the 16 elements per lane:
+// measured 4.4K cycles per layer epilogue).
+template <int ACT>
+__device__ __forceinline__ float act_t(float alpha, float x) {
 #ifdef GO2PI_DIAG_NOEPI
   return x;
 #endif
+  if constexpr (ACT == 1) return x > 0.f ? x : alpha * expm1_neg(x);  // Elu (ONNX opset 6)
+  else if constexpr (ACT == 2) return x > 0.f ? x : 0.f;              // Relu
+  else if constexpr (ACT == 3) return tanhf(x);                       // Tanh
+  else if constexpr (ACT == 4) return sigmoid_fast(x);                // Sigmoid
+  else if constexpr (ACT == 5) return x >= 0.f ? x : alpha * x;       // LeakyRelu
+  else return x;
+}
+
+__device__ __forceinline__ float act_fn(int act, float alpha, float x) {
   switch (act) {
-    case 1: return x > 0.f ? x : alpha * expm1_neg(x);         // Elu (ONNX opset 6)
-    case 2: return x > 0.f ? x : 0.f;                          // Relu
-    case 3: return tanhf(x);                                   // Tanh
-    case 4: return 1.f / (1.f + expf(-x));                     // Sigmoid
-    case 5: return x >= 0.f ? x : alpha * x;                   // LeakyRelu
-    default: return x;
+    case 1: return act_t<1>(alpha, x);
+    case 2: return act_t<2>(alpha, x);
+    case 3: return act_t<3>(alpha, x);
+    case 4: return act_t<4>(alpha, x);
+    case 5: return act_t<5>(alpha, x);
+    default: return act_t<0>(alpha, x);
+  }
+}
+
+// Calls f(std::integral_constant<int, ACT>) for the runtime activation kind.
+template <class F>
+__device__ __forceinline__ void with_act(int act, F &&f) {
+  switch (act) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    default: f(std::integral_constant<int, 0>{}); break;
   }
 }
 
@@ -118,17 +152,22 @@ __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, c
 #pragma unroll
   for (int i = 0; i < TPW; ++i) wp[i] = W + (size_t)min(t_first + i, T - 1) * 64 + lane;
   if (c0 >= c1) return;
-  const int cl = c1 - 1;
   float4 cur[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0, cs, i);
-  for (int c = c0; c < c1; c += 4) {
+  // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
+  // a trailing load would only be waited for by the epilogue
+  // (A operands are read per 4-chunk group; double-buffering them across groups
+  // measured slower: 100.4K vs 97.8K cycles per workgroup)
+  auto group = [&](int c, auto tail_k) {
+    constexpr bool TAIL = decltype(tail_k)::value;
     float4 a[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int cn = min(c + u + 1, cl);
+      const int cn = c + u + 1;
+      const bool LOAD = !(TAIL && u == 3);  // folded after unrolling
       float4 nxt[TPW];
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
@@ -136,14 +175,21 @@ __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, c
         acc[i] = mfma4(a[u].y, cur[i].y, acc[i]);
         acc[i] = mfma4(a[u].z, cur[i].z, acc[i]);
         acc[i] = mfma4(a[u].w, cur[i].w, acc[i]);
-        __builtin_amdgcn_sched_barrier(0);
-        nxt[i] = load_frag(wp[i], cn, cs, i);
-        __builtin_amdgcn_sched_barrier(0);
+        if (LOAD) {
+          __builtin_amdgcn_sched_barrier(0);
+          nxt[i] = load_frag(wp[i], cn, cs, i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
+      if (LOAD) {
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
+        for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
+      }
     }
-  }
+  };
+  int c = c0;
+  for (; c + 4 < c1; c += 4) group(c, std::false_type{});
+  group(c, std::true_type{});
 }
 
 // The bias is fetched before the contraction and added in the epilogue, so its
@@ -162,22 +208,26 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
                                             const float (&bv)[TPW], int t_first, int T, int lane, bool last, float *Y,
                                             int ys, float *out, int row0, int B) {
   const int col = lane & 15, r0 = (lane >> 4) << 2;
+  with_act(L.act, [&](auto act_k) {
+    constexpr int ACT = decltype(act_k)::value;
+    const float alpha = L.alpha;
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int t = t_first + i;
-    if (t >= T) continue;
-    const int n = t * 16 + col;
-    if (!last) {
+    for (int i = 0; i < TPW; ++i) {
+      const int t = t_first + i;
+      if (t >= T) continue;
+      const int n = t * 16 + col;
+      if (!last) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_fn(L.act, L.alpha, acc[i][r] + bv[i]);
-    } else if (n < L.N) {
+        for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_t<ACT>(alpha, acc[i][r] + bv[i]);
+      } else if (n < L.N) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = row0 + r0 + r;
-        if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_fn(L.act, L.alpha, acc[i][r] + bv[i]));
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + r0 + r;
+          if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_t<ACT>(alpha, acc[i][r] + bv[i]));
+        }
       }
     }
-  }
+  });
 }
 
 // HT > 0: "head fusion". The final, narrow layer HL (HT <= 2 output tiles, e.g.
@@ -204,8 +254,20 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
   }
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef GO2PI_DIAG_CLOCK  // per-wave phase stamps inside layer 1: entry, contraction done, epilogue done
+  unsigned long long *st = (P.stamps && &L == &P.L[1] && lane == 0)
+                               ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * (threadIdx.x >> 6)
+                               : nullptr;
+  if (st) st[0] = __builtin_amdgcn_s_memtime();
+#endif
   dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc);
+#ifdef GO2PI_DIAG_CLOCK
+  if (st) st[1] = __builtin_amdgcn_s_memtime();
+#endif
   dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, row0, B);
+#ifdef GO2PI_DIAG_CLOCK
+  if (st) st[2] = __builtin_amdgcn_s_memtime();
+#endif
   if constexpr (HT > 0) {
     // this wave's own LDS stores above are read back below (other lanes' values):
     // keep the compiler from hoisting the reads (the LDS queue is in order per wave)
@@ -243,7 +305,11 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   // largest tile group per pass: bounded so the accumulators fit the VGPR
   // budget of NW waves per CU (512 / (NW/4) registers per lane)
+#ifdef GO2PI_DIAG_G2
+  constexpr int G = 2;  // variant: smaller tile groups (epilogue of one group beside MFMAs of the next)
+#else
   constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
+#endif
   const int tpw = (T + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
@@ -398,8 +464,8 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = r0 + e;
-      const float zg = 1.f / (1.f + expf(-z[i][e]));
-      const float rg = 1.f / (1.f + expf(-r[i][e]));
+      const float zg = sigmoid_fast(z[i][e]);
+      const float rg = sigmoid_fast(r[i][e]);
       const float hn = tanhf(nx[i][e] + rg * nh[i][e]);
       const float ho = Hs[row * xs + j];
       Y[row * xs + j] = (1.f - zg) * hn + zg * ho;
@@ -437,6 +503,14 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
   const int H = P.gru.H;
+  // Touch every layer descriptor up front: one burst of scalar loads warms the
+  // scalar cache, so each layer's start does not pay a K$ miss on its fields
+  // (measured: layer entry ~990 -> ~740 cycles after the barrier).
+  {
+    int d = 0;
+    for (int l = 0; l < P.nl; ++l) d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w;
+    asm volatile("" ::"s"(d));  // consumes the loads; no side effect
+  }
 #ifdef GO2PI_DIAG_CLOCK
   if (tid == 0 && P.stamps) {
     P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();

@@ -21,7 +21,7 @@
 #define GO2PI_MAX_LAYERS 8
 #define GO2PI_TILE_ROWS 16      // robots per workgroup tile in the batched kernel
 #define GO2PI_SMALL_MAXB 8      // max rows of the GEMV chain
-#define GO2PI_STAMPS_PER_WG 16  // diagnostics: {start, end} x {memtime, realtime} + 12 phase memtimes
+#define GO2PI_STAMPS_PER_WG 64  // diagnostics: {start,end} x {memtime,realtime}, phase marks, per-wave layer-1 marks
 
 namespace go2pi {
 

@@ -38,8 +38,16 @@ def main():
             e.run_torch(x, out=y, stream=s)
         n += 50
         s.synchronize()
-    st = e.diag_stamps(16 * ((args.batch + 15) // 16)).reshape(-1, 16).astype(np.float64)
+    SPW = 64
+    st = e.diag_stamps(SPW * ((args.batch + 15) // 16)).reshape(-1, SPW).astype(np.float64)
     nl = e.cost["n_layers"]
+    # per-wave layer-1 marks (slots 16 + 3w + {0,1,2}), relative to the layer-0 barrier (slot 6)
+    waves_l1 = {}
+    for w in range(min(args.waves, 16)):
+        s0, s1, s2 = st[:, 16 + 3 * w], st[:, 17 + 3 * w], st[:, 18 + 3 * w]
+        if np.all(s0 > 0):
+            waves_l1[w] = [float(np.median(s0 - st[:, 6])), float(np.median(s1 - st[:, 6])),
+                           float(np.median(s2 - st[:, 6])), float(np.median(st[:, 7] - st[:, 6]))]
     marks = [st[:, 0], st[:, 4]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
     names = ["init"] + [f"layer{l}" for l in range(nl)] + ["tail"]
     phases = {n: float(np.median(b - a)) for n, a, b in zip(names, marks[:-1], marks[1:])}
@@ -51,7 +59,8 @@ def main():
            "clock_ghz_min": float(clk.min() / 1e9), "wg_cycles_median": float(np.median(cyc)),
            "wg_us_median": float(np.median(rt) * 1e6), "wg_us_max": float(rt.max() * 1e6),
            "launch_span_us": float((st[:, 3].max() - st[:, 1].min()) / 100),
-           "phase_cycles_median": phases}
+           "phase_cycles_median": phases,
+           "layer1_wave_marks": waves_l1}  # [entry, contraction done, epilogue done, barrier] cycles
     print(json.dumps(out))
 
 
