@@ -403,61 +403,55 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
     wp[i] = W + (size_t)(t_first + i) * 192 + lane;
   }
   const int cs = (G.H >> 4) * 192;  // chunk-major: [chunk][tile][gate][lane]
-  (void)Cc;
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
-  for (int c = 0; c < Cx; ++c) {
-    const float4 a = *reinterpret_cast<const float4 *>(xrow + c * 16);
-    float4 wz[GT], wr[GT], wh[GT];
+  // One stream over the concatenated [x | h] chunks, scheduled like dense_acc:
+  // each gate fragment of chunk c+1 is loaded right after that gate's 4 MFMAs
+  // of chunk c (x chunks feed z, r, n_x; h chunks feed z, r, n_h).
+  float4 cz[GT], cr[GT], chh[GT];
 #pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      wz[i] = wp[i][c * cs];
-      wr[i] = wp[i][c * cs + 64];
-      wh[i] = wp[i][c * cs + 128];
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.x, wz[i].x, z[i]); r[i] = mfma4(a.x, wr[i].x, r[i]); nx[i] = mfma4(a.x, wh[i].x, nx[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.y, wz[i].y, z[i]); r[i] = mfma4(a.y, wr[i].y, r[i]); nx[i] = mfma4(a.y, wh[i].y, nx[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.z, wz[i].z, z[i]); r[i] = mfma4(a.z, wr[i].z, r[i]); nx[i] = mfma4(a.z, wh[i].z, nx[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.w, wz[i].w, z[i]); r[i] = mfma4(a.w, wr[i].w, r[i]); nx[i] = mfma4(a.w, wh[i].w, nx[i]);
-    }
+  for (int i = 0; i < GT; ++i) {
+    cz[i] = wp[i][0];
+    cr[i] = wp[i][64];
+    chh[i] = wp[i][128];
   }
-  for (int c = 0; c < Ch; ++c) {
-    const float4 a = *reinterpret_cast<const float4 *>(hrow + c * 16);
-    float4 wz[GT], wr[GT], wh[GT];
+  auto step = [&](int c, const float4 &a, f32x4 (&third)[GT], int cn) {
+    float4 nz[GT], nr[GT], nh3[GT];
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
-      wz[i] = wp[i][(Cx + c) * cs];
-      wr[i] = wp[i][(Cx + c) * cs + 64];
-      wh[i] = wp[i][(Cx + c) * cs + 128];
+      z[i] = mfma4(a.x, cz[i].x, z[i]);
+      z[i] = mfma4(a.y, cz[i].y, z[i]);
+      z[i] = mfma4(a.z, cz[i].z, z[i]);
+      z[i] = mfma4(a.w, cz[i].w, z[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      nz[i] = wp[i][cn * cs];
+      __builtin_amdgcn_sched_barrier(0);
+      r[i] = mfma4(a.x, cr[i].x, r[i]);
+      r[i] = mfma4(a.y, cr[i].y, r[i]);
+      r[i] = mfma4(a.z, cr[i].z, r[i]);
+      r[i] = mfma4(a.w, cr[i].w, r[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      nr[i] = wp[i][cn * cs + 64];
+      __builtin_amdgcn_sched_barrier(0);
+      third[i] = mfma4(a.x, chh[i].x, third[i]);
+      third[i] = mfma4(a.y, chh[i].y, third[i]);
+      third[i] = mfma4(a.z, chh[i].z, third[i]);
+      third[i] = mfma4(a.w, chh[i].w, third[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      nh3[i] = wp[i][cn * cs + 128];
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.x, wz[i].x, z[i]); r[i] = mfma4(a.x, wr[i].x, r[i]); nh[i] = mfma4(a.x, wh[i].x, nh[i]);
+      cz[i] = nz[i];
+      cr[i] = nr[i];
+      chh[i] = nh3[i];
     }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.y, wz[i].y, z[i]); r[i] = mfma4(a.y, wr[i].y, r[i]); nh[i] = mfma4(a.y, wh[i].y, nh[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.z, wz[i].z, z[i]); r[i] = mfma4(a.z, wr[i].z, r[i]); nh[i] = mfma4(a.z, wh[i].z, nh[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.w, wz[i].w, z[i]); r[i] = mfma4(a.w, wr[i].w, r[i]); nh[i] = mfma4(a.w, wh[i].w, nh[i]);
-    }
-  }
+    (void)c;
+  };
+  for (int c = 0; c < Cx; ++c) step(c, *reinterpret_cast<const float4 *>(xrow + c * 16), nx, c + 1);
+  for (int c = 0; c < Ch; ++c)
+    step(Cx + c, *reinterpret_cast<const float4 *>(hrow + c * 16), nh, min(Cx + c + 1, Cc - 1));
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
     const int j = (t_first + i) * 16 + col;
@@ -466,7 +460,7 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
       const int row = r0 + e;
       const float zg = sigmoid_fast(z[i][e]);
       const float rg = sigmoid_fast(r[i][e]);
-      const float hn = tanhf(nx[i][e] + rg * nh[i][e]);
+      const float hn = 2.f * sigmoid_fast(2.f * (nx[i][e] + rg * nh[i][e])) - 1.f;  // tanh, ~1e-7 abs
       const float ho = Hs[row * xs + j];
       Y[row * xs + j] = (1.f - zg) * hn + zg * ho;
     }
