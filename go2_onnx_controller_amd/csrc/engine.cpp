@@ -83,6 +83,11 @@ struct go2pi_engine {
   bool done_ok = false;                            // final layer is one tile: WG 0 signals completion
   go2pi::DevProgram *d_prog = nullptr;             // device copy of prog (latency kernel argument)
   unsigned epoch = 1, last_epoch = 0;
+  // controller tick (go2pi_controller_step*)
+  int ctl_hist = 0;                        // kHistory when the policy's I/O is a Go2 controller's, else 0
+  go2pi::DevCtlParams *d_ctl = nullptr;    // device copy of the parameters
+  char *h_ctl = nullptr, *m_ctl = nullptr; // host path, batch <= SMALL_MAXB: pinned host-mapped staging
+  char *d_ctlbuf = nullptr;                // host path, larger batches: device staging (lazy)
 
   ~go2pi_engine() {
     (void)hipSetDevice(device);
@@ -95,6 +100,7 @@ struct go2pi_engine {
     if (h_obs) (void)hipHostFree(h_obs);
     if (h_act) (void)hipHostFree(h_act);
     if (h_err) (void)hipHostFree(h_err);
+    if (h_ctl) (void)hipHostFree(h_ctl);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -120,17 +126,53 @@ struct go2pi_engine {
 
   // Enqueue one forward over `batch` rows (obs/act: device-accessible pointers).
   // done (single-launch path only): host-mapped word the kernel sets to the call's epoch.
+  // granule tags of the next single-launch call (layer l of this call: e0 + l)
+  unsigned next_epoch(hipStream_t s) {
+    const unsigned n = (unsigned)prog.nl;
+    if (epoch > 0xFFFFFFFFu - 2 * n) {  // tag space exhausted (~1e9 calls): clear granules, restart
+      hip_check(hipMemsetAsync(d_gran, 0, sizeof(unsigned long long) * (size_t)(prog.nl - 1) * gstride, s),
+                "hipMemsetAsync");
+      epoch = 1;
+    }
+    const unsigned e0 = epoch;
+    epoch += n;
+    last_epoch = e0;
+    return e0;
+  }
+
+  // Host spin on the host-mapped completion word of the single-launch path;
+  // false: not observed within 2 s (the caller falls back to a stream sync).
+  bool spin_done() {
+    const unsigned want = last_epoch;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0; __atomic_load_n(h_done, __ATOMIC_ACQUIRE) != want; ++it) {
+      __builtin_ia32_pause();
+      if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    return __atomic_load_n(h_done, __ATOMIC_ACQUIRE) == want;
+  }
+
+  void check_handoff() {
+    if (h_err && __atomic_load_n(h_err, __ATOMIC_ACQUIRE)) {
+      __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
+      throw HipError("batch-1 kernel hand-off timed out (workgroups not co-resident?)", GO2PI_E_DEVICE);
+    }
+  }
+
+  // Enqueue one controller tick (device-accessible pointers in c).
+  void enqueue_ctl(const go2pi::DevCtl &c, int64_t batch, hipStream_t s, unsigned *done = nullptr) {
+    if (use_latency(batch) && done_ok) {
+      const unsigned e0 = next_epoch(s);
+      hip_check(go2pi::launch_latency_ctl(prog, d_prog, c, (int)batch, e0, d_gran, gstride, m_err, done, s),
+                "controller latency launch");
+    } else {
+      hip_check(go2pi::launch_policy_fused_ctl(prog, waves, c, d_hidden, (int)batch, s), "controller fused launch");
+    }
+  }
+
   void enqueue(const float *obs, float *act, int64_t batch, hipStream_t s, unsigned *done = nullptr) {
     if (use_latency(batch)) {
-      const unsigned n = (unsigned)prog.nl;
-      if (epoch > 0xFFFFFFFFu - 2 * n) {  // tag space exhausted (~1e9 calls): clear granules, restart
-        hip_check(hipMemsetAsync(d_gran, 0, sizeof(unsigned long long) * (size_t)(prog.nl - 1) * gstride, s),
-                  "hipMemsetAsync");
-        epoch = 1;
-      }
-      const unsigned e0 = epoch;
-      epoch += n;
-      last_epoch = e0;
+      const unsigned e0 = next_epoch(s);
       hip_check(go2pi::launch_latency(prog, d_prog, obs, act, (int)batch, e0, d_gran, gstride, m_err, done, s),
                 "latency launch");
     } else if (use_chain(batch)) {
@@ -210,6 +252,20 @@ void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
             }
             w[((((size_t)c * Ht + t) * 3 + gate) * 64 + lane) * 4 + j] = v;
           }
+}
+
+void set_ctl_params(go2pi_engine &e, const go2pi_ctl_params &cp) {
+  go2pi::DevCtlParams d{};
+  for (int i = 0; i < GO2PI_CTL_DOF; ++i) d.q0[i] = cp.q0[i];
+  d.action_scale = cp.action_scale;
+  d.kp_run = (double)cp.kp;  // float members widened at send_command (controller.cpp:246-247)
+  d.kd_run = (double)cp.kd;
+  d.kp_stop = (double)cp.kp_stop;
+  d.action_limit = cp.action_limit;
+  d.contact_threshold = cp.contact_threshold;
+  for (int i = 0; i < 3; ++i) d.gravity_w[i] = cp.gravity_w[i];
+  d.hist = e.ctl_hist;
+  hip_check(hipMemcpy(e.d_ctl, &d, sizeof(d), hipMemcpyHostToDevice), "hipMemcpy");
 }
 
 void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o) {
@@ -383,6 +439,14 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     hip_check(hipMemset(p.stamps, 0, e.n_stamps * sizeof(unsigned long long)), "hipMemset");
   }
   // the finished program, copied to device memory for the latency kernel
+  // controller tick: a policy with kHistory x 49 observations and 12 actions
+  if (m.in_dim > 0 && m.in_dim % GO2PI_CTL_STEP_DIM == 0 && m.out_dim == GO2PI_CTL_DOF) {
+    e.ctl_hist = m.in_dim / GO2PI_CTL_STEP_DIM;
+    e.d_ctl = e.dalloc<go2pi::DevCtlParams>(1);
+    go2pi_ctl_params cp;
+    go2pi_ctl_default_params(&cp);
+    set_ctl_params(e, cp);
+  }
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -537,25 +601,14 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
         // one direct launch (per-call epoch argument); completion observed by spinning on
         // the host-mapped done word (a stream sync costs ~10 us more on this stack)
         e->enqueue(e->m_obs, e->m_act, batch, e->stream, e->done_ok ? e->m_done : nullptr);
-        if (e->done_ok) {
-          const unsigned want = e->last_epoch;
-          const auto t0 = std::chrono::steady_clock::now();
-          for (unsigned it = 0; __atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) != want; ++it) {
-            __builtin_ia32_pause();
-            if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
-          }
-          synced = __atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) == want;
-        }
+        if (e->done_ok) synced = e->spin_done();
       } else if (!e->opts.use_graph) {
         e->enqueue(e->m_obs, e->m_act, batch, e->stream);
       } else {
         hip_check(hipGraphLaunch(e->graph_for((int)batch), e->stream), "hipGraphLaunch");
       }
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-      if (e->h_err && __atomic_load_n(e->h_err, __ATOMIC_ACQUIRE)) {
-        __atomic_store_n(e->h_err, 0u, __ATOMIC_RELEASE);
-        throw HipError("batch-1 kernel hand-off timed out (workgroups not co-resident?)", GO2PI_E_DEVICE);
-      }
+      e->check_handoff();
       std::memcpy(act, e->h_act, out_b);
     } else {
       hip_check(hipMemcpyAsync(e->d_obs, obs, in_b, hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync H2D");
@@ -655,6 +708,161 @@ int go2pi_set_hidden(go2pi_engine *e, const float *h, int64_t batch) {
     hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
     hip_check(hipMemcpy(e->d_hidden, h, sizeof(float) * (size_t)batch * e->model.gru.H, hipMemcpyHostToDevice),
               "hipMemcpy H2D");
+    return GO2PI_OK;
+  });
+}
+
+void go2pi_ctl_default_params(go2pi_ctl_params *p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->struct_size = sizeof(go2pi_ctl_params);
+  p->kp = 28.f;  // controller.hpp:119-120
+  p->kd = 0.5f;
+  p->kp_stop = 5.f;           // controller.cpp:246
+  p->action_limit = 1000.f;   // kActionLimit, controller.hpp:17
+  p->contact_threshold = 22.f;  // controller.hpp:100-103
+  p->gravity_w[2] = -1.f;     // gravity_w_, controller.hpp:131
+  p->action_scale = 0.25;     // controller.cpp:244
+  static const double q0[12] = {0.1, -0.1, 0.1, -0.1, 0.8, 0.8, 1.0, 1.0, -1.5, -1.5, -1.5, -1.5};  // controller.hpp:165
+  std::memcpy(p->q0, q0, sizeof(q0));
+}
+
+int go2pi_ctl_history(const go2pi_engine *e, int32_t *hist) {
+  return guarded([&] {
+    check_engine(e);
+    if (!e->ctl_hist)
+      throw ApiError("policy I/O is not a Go2 controller's (obs " + std::to_string(e->model.in_dim) +
+                         " not a multiple of 49, or action " + std::to_string(e->model.out_dim) + " != 12)",
+                     GO2PI_E_MODEL);
+    if (hist) *hist = e->ctl_hist;
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_ctl_set_params(go2pi_engine *e, const go2pi_ctl_params *p) {
+  return guarded([&] {
+    check_engine(e);
+    if (!p) throw ApiError("null params", GO2PI_E_INVALID);
+    if (p->struct_size != (int32_t)sizeof(go2pi_ctl_params))
+      throw ApiError("go2pi_ctl_params.struct_size mismatch", GO2PI_E_INVALID);
+    if (!e->ctl_hist) throw ApiError("policy I/O is not a Go2 controller's", GO2PI_E_MODEL);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    set_ctl_params(*e, *p);
+    return GO2PI_OK;
+  });
+}
+
+namespace {
+// byte offsets of the controller staging buffers for `rows` robots (256 B aligned)
+struct CtlLayout {
+  size_t state, joy, obs, action, q_des, kp, kd, status, total;
+  CtlLayout(int64_t rows, int in_dim) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    state = o; o = al(o + sizeof(float) * rows * GO2PI_CTL_STATE_DIM);
+    joy = o; o = al(o + sizeof(float) * rows * GO2PI_CTL_JOY_DIM);
+    obs = o; o = al(o + sizeof(float) * rows * in_dim);
+    action = o; o = al(o + sizeof(float) * rows * GO2PI_CTL_DOF);
+    q_des = o; o = al(o + sizeof(double) * rows * GO2PI_CTL_DOF);
+    kp = o; o = al(o + sizeof(double) * rows * GO2PI_CTL_DOF);
+    kd = o; o = al(o + sizeof(double) * rows * GO2PI_CTL_DOF);
+    status = o; o = al(o + sizeof(uint32_t) * rows);
+    total = o;
+  }
+};
+
+void check_ctl(const go2pi_engine *e, int64_t batch) {
+  check_engine(e);
+  check_batch(e, batch);
+  if (!e->ctl_hist) throw ApiError("policy I/O is not a Go2 controller's (need 49*k obs, 12 actions)", GO2PI_E_MODEL);
+}
+}  // namespace
+
+int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy, float *obs, float *action,
+                          double *q_des, double *kp, double *kd, uint32_t *status, int64_t batch) {
+  return guarded([&] {
+    check_ctl(e, batch);
+    if (batch == 0) return GO2PI_OK;
+    if (!state || !obs || !action) throw ApiError("null state/obs/action buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    const int in_dim = e->model.in_dim;
+    const bool small = batch <= GO2PI_SMALL_MAXB;
+    const CtlLayout L(small ? GO2PI_SMALL_MAXB : e->opts.max_batch, in_dim);
+    const size_t n_state = sizeof(float) * batch * GO2PI_CTL_STATE_DIM, n_joy = sizeof(float) * batch * GO2PI_CTL_JOY_DIM;
+    const size_t n_obs = sizeof(float) * batch * in_dim, n_act = sizeof(float) * batch * GO2PI_CTL_DOF;
+    const size_t n_d = sizeof(double) * batch * GO2PI_CTL_DOF, n_st = sizeof(uint32_t) * batch;
+    char *dev;  // device-side view of the staging
+    if (small) {
+      if (!e->h_ctl) {
+        hip_check(hipHostMalloc((void **)&e->h_ctl, L.total, hipHostMallocMapped | hipHostMallocCoherent),
+                  "hipHostMalloc");
+        hip_check(hipHostGetDevicePointer((void **)&e->m_ctl, e->h_ctl, 0), "hipHostGetDevicePointer");
+      }
+      std::memcpy(e->h_ctl + L.state, state, n_state);
+      if (joy) std::memcpy(e->h_ctl + L.joy, joy, n_joy);
+      std::memcpy(e->h_ctl + L.obs, obs, n_obs);
+      std::memcpy(e->h_ctl + L.action, action, n_act);
+      dev = e->m_ctl;
+    } else {
+      if (!e->d_ctlbuf) e->d_ctlbuf = e->dalloc<char>(L.total);
+      dev = e->d_ctlbuf;
+      auto h2d = [&](size_t off, const void *src, size_t n) {
+        hip_check(hipMemcpyAsync(dev + off, src, n, hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync H2D");
+      };
+      h2d(L.state, state, n_state);
+      if (joy) h2d(L.joy, joy, n_joy);
+      h2d(L.obs, obs, n_obs);
+      h2d(L.action, action, n_act);
+    }
+    go2pi::DevCtl c{};
+    c.prm = e->d_ctl;
+    c.state = reinterpret_cast<const float *>(dev + L.state);
+    c.joy = joy ? reinterpret_cast<const float *>(dev + L.joy) : nullptr;
+    c.obs = reinterpret_cast<float *>(dev + L.obs);
+    c.action = reinterpret_cast<float *>(dev + L.action);
+    c.q_des = q_des ? reinterpret_cast<double *>(dev + L.q_des) : nullptr;
+    c.kp = kp ? reinterpret_cast<double *>(dev + L.kp) : nullptr;
+    c.kd = kd ? reinterpret_cast<double *>(dev + L.kd) : nullptr;
+    c.status = status ? reinterpret_cast<uint32_t *>(dev + L.status) : nullptr;
+    const bool single = small && e->use_latency(batch) && e->done_ok;
+    e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
+    if (small) {
+      const bool synced = single && e->spin_done();
+      if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      e->check_handoff();
+      std::memcpy(obs, e->h_ctl + L.obs, n_obs);
+      std::memcpy(action, e->h_ctl + L.action, n_act);
+      if (q_des) std::memcpy(q_des, e->h_ctl + L.q_des, n_d);
+      if (kp) std::memcpy(kp, e->h_ctl + L.kp, n_d);
+      if (kd) std::memcpy(kd, e->h_ctl + L.kd, n_d);
+      if (status) std::memcpy(status, e->h_ctl + L.status, n_st);
+    } else {
+      auto d2h = [&](void *dst, size_t off, size_t n) {
+        hip_check(hipMemcpyAsync(dst, dev + off, n, hipMemcpyDeviceToHost, e->stream), "hipMemcpyAsync D2H");
+      };
+      d2h(obs, L.obs, n_obs);
+      d2h(action, L.action, n_act);
+      if (q_des) d2h(q_des, L.q_des, n_d);
+      if (kp) d2h(kp, L.kp, n_d);
+      if (kd) d2h(kd, L.kd, n_d);
+      if (status) d2h(status, L.status, n_st);
+      hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    }
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_controller_step_device(go2pi_engine *e, const float *state, const float *joy, float *obs, float *action,
+                                 double *q_des, double *kp, double *kd, uint32_t *status, int64_t batch,
+                                 void *hip_stream) {
+  return guarded([&] {
+    check_ctl(e, batch);
+    if (batch == 0) return GO2PI_OK;
+    if (!state || !obs || !action) throw ApiError("null state/obs/action buffer", GO2PI_E_INVALID);
+    hip_check(hipSetDevice(e->device), "hipSetDevice");
+    go2pi::DevCtl c{e->d_ctl, state, joy, obs, action, q_des, kp, kd, status};
+    e->enqueue_ctl(c, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
   });
 }

@@ -116,6 +116,103 @@ __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
 }
 
 // ---------------------------------------------------------------------------
+// Controller tick. The observation is the concatenation
+// of seven history blocks (controller.cpp:210-212); block b holds kHistory
+// copies of a d_b-wide signal, oldest first, and each tick shifts it left by
+// d_b and appends the current value (populate_buffer, controller.hpp:45-52).
+// Blocks: gravity_b 3, base_ang_vel 3, vel_cmd 3, q - q0 12, dq 12, previous
+// action 12, foot contacts 4 (cumulative 0,3,6,9,21,33,45; 49 per step).
+__device__ __forceinline__ void ctl_block(int H, int k, int &b, int &j, int &d) {
+  const int u = k / H;  // position in the 49-wide per-step layout
+  int c;
+  if (u < 9) { b = u / 3; c = 3 * b; d = 3; }
+  else if (u < 45) { b = 3 + (u - 9) / 12; c = 9 + 12 * (b - 3); d = 12; }
+  else { b = 6; c = 45; d = 4; }
+  j = k - H * c;
+}
+
+// gravity_b = quaternion_.inverse() * gravity_w_ (controller.cpp:182-184) with
+// Eigen 3.4 semantics: inverse() = conjugate / squaredNorm (the zero quaternion
+// if squaredNorm <= 0), squaredNorm summed as (x²+z²)+(y²+w²) (SSE predux of
+// the (x,y,z,w) coefficients), and q * v = _transformVector:
+// uv = 2 (q.vec × v), r = (v + w uv) + q.vec × uv. Every operation rounds to
+// fp32 in that order (no fma contraction), like the reference's x86 build.
+__device__ __forceinline__ float ctl_gravity(const float *st, const float *gw, int i) {
+#pragma clang fp contract(off)
+  const float w = st[0], x = st[1], y = st[2], z = st[3];
+  const float n2 = (x * x + z * z) + (y * y + w * w);
+  float qw = 0.f, qx = 0.f, qy = 0.f, qz = 0.f;
+  if (n2 > 0.f) {
+    qx = -x / n2;
+    qy = -y / n2;
+    qz = -z / n2;
+    qw = w / n2;
+  }
+  const float v0 = gw[0], v1 = gw[1], v2 = gw[2];
+  float u0 = qy * v2 - qz * v1, u1 = qz * v0 - qx * v2, u2 = qx * v1 - qy * v0;
+  u0 += u0;
+  u1 += u1;
+  u2 += u2;
+  const float c0 = qy * u2 - qz * u1, c1 = qz * u0 - qx * u2, c2 = qx * u1 - qy * u0;
+  if (i == 0) return (v0 + qw * u0) + c0;
+  if (i == 1) return (v1 + qw * u1) + c1;
+  return (v2 + qw * u2) + c2;
+}
+
+// Raw (un-normalised) observation feature k of robot `row` for this tick.
+// Reads the previous tick's observation (history) and action; obs is updated
+// in place by the caller only after every read of the tile is done.
+__device__ __forceinline__ float ctl_obs_value(const DevCtl &C, int in_dim, int row, int k) {
+  const DevCtlParams &Q = *C.prm;
+  const int H = Q.hist;
+  int b, j, d;
+  ctl_block(H, k, b, j, d);
+  const float *orow = C.obs + (size_t)row * in_dim;
+  if (j < (H - 1) * d) return orow[k + d];  // shifted history
+  const int i = j - (H - 1) * d;
+  const float *st = C.state + (size_t)row * GO2PI_CTL_STATE_DIM;
+  switch (b) {
+    case 0: return ctl_gravity(st, Q.gravity_w, i);
+    case 1: return st[4 + i];  // imu gyroscope (controller.hpp:105-109)
+    case 2: {                  // vel_cmd from the joystick (controller.cpp:173-179), sticky without one
+      const float *jy = C.joy ? C.joy + (size_t)row * GO2PI_CTL_JOY_DIM : nullptr;
+      if (!jy || jy[0] == 0.f) return orow[k];  // previous tick's vel_cmd_
+      if (i == 0) return jy[2];                 // axes[1]
+      if (i == 2) return jy[3] * jy[2];         // axes[3] * axes[1]
+      const double a0 = jy[1];                  // pow(axes[0], 2) * sign * 0.8, in double
+      return (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
+    }
+    case 3: return (float)((double)st[7 + i] - Q.q0[i]);  // q_[i] -= q0_[i] (double q0_)
+    case 4: return st[19 + i];
+    case 5: return C.action[(size_t)row * GO2PI_CTL_DOF + i];  // action_ before act()
+    default:  // contacts: foot_force >= 22 with the FR/FL, RR/RL swap (controller.hpp:99-103)
+      return st[31 + (i ^ 1)] >= Q.contact_threshold ? 1.f : 0.f;
+  }
+}
+
+// Features the reference checks after each single-signal populate_buffer: a
+// NaN there makes it exit(1) (controller.hpp:57-64); flagged in status here.
+__device__ __forceinline__ bool ctl_checked(int H, int k) {
+  int b, j, d;
+  ctl_block(H, k, b, j, d);
+  return b < 6 && j >= (H - 1) * d;
+}
+
+// Action post-processing of robot `row`, joint n (controller.cpp:217-223, 240-248).
+__device__ __forceinline__ void ctl_store(const DevCtl &C, int row, int n, float v) {
+  const DevCtlParams &Q = *C.prm;
+  const float lim = Q.action_limit;
+  float a = v < -lim ? -lim : (lim < v ? lim : v);  // std::clamp (NaN passes through)
+  const bool stop = C.joy && C.joy[(size_t)row * GO2PI_CTL_JOY_DIM + 4] != 0.f;
+  a *= stop ? 0.f : 1.f;  // a *= joy_->buttons[0] == 0
+  const size_t o = (size_t)row * GO2PI_CTL_DOF + n;
+  C.action[o] = a;
+  if (C.q_des) C.q_des[o] = Q.q0[n] + (double)a * Q.action_scale;
+  if (C.kp) C.kp[o] = stop ? Q.kp_stop : Q.kp_run;
+  if (C.kd) C.kd[o] = Q.kd_run;
+}
+
+// ---------------------------------------------------------------------------
 // Dense contraction over k-chunks [c0, c1) for TPW consecutive 16-col tiles.
 // X: LDS activations [16][xs], W: this layer's fragments (chunk-major: the
 // float4 stride between consecutive chunks of one tile is TL * 64).
@@ -206,7 +303,7 @@ __device__ __forceinline__ void load_bias(float (&bv)[TPW], const float *__restr
 template <int TPW>
 __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW],
                                             const float (&bv)[TPW], int t_first, int T, int lane, bool last, float *Y,
-                                            int ys, float *out, int row0, int B) {
+                                            int ys, float *out, const DevCtl *ctl, int row0, int B) {
   const int col = lane & 15, r0 = (lane >> 4) << 2;
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
@@ -223,7 +320,10 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = row0 + r0 + r;
-          if (row < B) out[(size_t)row * L.N + n] = post_fn(P, act_t<ACT>(alpha, acc[i][r] + bv[i]));
+          if (row >= B) continue;
+          const float v = post_fn(P, act_t<ACT>(alpha, acc[i][r] + bv[i]));
+          if (ctl) ctl_store(*ctl, row, n, v);  // controller tick: action post-processing
+          else out[(size_t)row * L.N + n] = v;
         }
       }
     }
@@ -237,8 +337,9 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
 // Partials are summed across waves in a fixed order by head_finish (below).
 template <int TPW, int HT>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int t_first, int T, int C, int lane, bool last, float *out, int row0,
-                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+                                            int t_first, int T, int C, int lane, bool last, float *out,
+                                            const DevCtl *ctl, int row0, int B, const DevLayer *HL,
+                                            f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   constexpr int HN = HT > 0 ? HT : 1;
   f32x4 acc[TPW];
   float bv[TPW];
@@ -264,7 +365,7 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 #ifdef GO2PI_DIAG_CLOCK
   if (st) st[1] = __builtin_amdgcn_s_memtime();
 #endif
-  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, row0, B);
+  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, ctl, row0, B);
 #ifdef GO2PI_DIAG_CLOCK
   if (st) st[2] = __builtin_amdgcn_s_memtime();
 #endif
@@ -290,18 +391,18 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 
 template <int TPW>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int t_first, int T, int C, int lane, bool last, float *out, int row0,
-                                            int B) {
+                                            int t_first, int T, int C, int lane, bool last, float *out,
+                                            const DevCtl *ctl, int row0, int B) {
   f32x4 none[1];
-  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, row0, B, nullptr, none);
+  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none);
 }
 
 // Tiles of a wide layer split over the NW waves (full K per wave), optionally
 // with the fused head (HT > 0). Barrier-free.
 template <int NW, int HT>
 __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int wave, int lane, bool last, float *out, int row0, int B,
-                                            const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+                                            int wave, int lane, bool last, float *out, const DevCtl *ctl, int row0,
+                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   // largest tile group per pass: bounded so the accumulators fit the VGPR
   // budget of NW waves per CU (512 / (NW/4) registers per lane)
@@ -313,13 +414,13 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
   const int tpw = (T + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
-  for (; t + G <= t_end; t += G) dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, row0, B, HL, hacc);
+  for (; t + G <= t_end; t += G) dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc);
   const int rem = t_end - t;
-  if (G > 4 && rem > 4) dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+  if (G > 4 && rem > 4) dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
   else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
-  else if (rem == 2) dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
-  else if (rem == 1) dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, row0, B, HL, hacc);
+    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
+  else if (rem == 2) dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
+  else if (rem == 1) dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
 }
 
 // Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
@@ -331,33 +432,33 @@ __device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevL
   f32x4 hacc[HT];
 #pragma unroll
   for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, row0, B, &HL, hacc);
+  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, nullptr, row0, B, &HL, hacc);
 #pragma unroll
   for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
 }
 
 template <int NW>
 __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer &HL, const f32x4 *scratch, int wave,
-                                            int lane, float *out, int row0, int B) {
+                                            int lane, float *out, const DevCtl *ctl, int row0, int B) {
   const int T = HL.N_pad >> 4;
   if (wave >= T) return;
   f32x4 acc[1] = {scratch[(wave * NW) * 64 + lane]};
   for (int w = 1; w < NW; ++w) acc[0] += scratch[(wave * NW + w) * 64 + lane];  // fixed order: deterministic
   float bv[1];
   load_bias<1>(bv, HL.bias, wave, T, lane);
-  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, row0, B);
+  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, ctl, row0, B);
 }
 
 // One dense layer for the whole workgroup (NW waves). Contains barriers only in
 // the split-K branch, which every wave of the workgroup takes together.
 template <int NW>
 __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            f32x4 *scratch, int wave, int lane, bool last, float *out, int row0,
-                                            int B) {
+                                            f32x4 *scratch, int wave, int lane, bool last, float *out,
+                                            const DevCtl *ctl, int row0, int B) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
     f32x4 none[1];
-    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, row0, B, nullptr, none);
+    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none);
   } else {
     // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
     const int ks = NW / T;
@@ -375,7 +476,7 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
     __syncthreads();
     if (s == 0) {
       for (int s2 = 1; s2 < ks; ++s2) acc[0] += scratch[(t + s2 * T) * 64 + lane];
-      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, row0, B);
+      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, ctl, row0, B);
     }
   }
 }
@@ -481,10 +582,13 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
   for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
 }
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
-                                                               float *__restrict__ act, float *__restrict__ hidden,
-                                                               int B, int steps) {
+// Body of the batched kernel. CTL: controller tick (steps == 1) — the
+// observation is assembled from raw robot state (ctl_obs_value) instead of
+// read, and the final layer's store is the action post-processing (ctl_store).
+template <int NW, bool CTL>
+__device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
+                                           float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
+                                           const DevCtl *ctl) {
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   const int S = P.lds_stride;
@@ -517,7 +621,14 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
     for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
       const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
       float v = 0.f;
-      if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
+      if constexpr (CTL) {  // raw value; written back to ctl->obs and normalised after the barrier
+        if (row < B && k < P.in_dim) {
+          v = ctl_obs_value(*ctl, P.in_dim, row, k);
+          if (k == 0 && ctl->status) ctl->status[row] = 0u;
+        }
+      } else {
+        if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
+      }
       bufA[r * S + k] = v;
     }
   };
@@ -548,6 +659,20 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
     float *ac = act + (size_t)step * B * P.out_dim;
     if (step > 0) stage_obs(step);
     __syncthreads();
+    if constexpr (CTL) {
+      // every read of this tile's previous obs / action happened before the barrier:
+      // publish the new observation (the ObservationAction log, controller.cpp:226)
+      const bool norm = P.pre_sub || P.pre_div || P.obs_clip > 0.f;
+      for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
+        const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
+        if (row >= B || k >= P.in_dim) continue;
+        const float v = bufA[r * S + k];
+        ctl->obs[(size_t)row * P.in_dim + k] = v;
+        if (ctl->status && __builtin_isnan(v) && ctl_checked(ctl->prm->hist, k)) atomicOr(ctl->status + row, 1u);
+        if (norm) bufA[r * S + k] = prologue(P, v, k);
+      }
+      if (norm) __syncthreads();
+    }
 #ifdef GO2PI_DIAG_CLOCK
     if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -570,7 +695,7 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
         if (P.head_fuse == 1) dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
         else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
         __syncthreads();
-        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, row0, B);
+        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, ctl, row0, B);
 #ifdef GO2PI_DIAG_CLOCK
         if (tid == 0 && P.stamps && step == 0 && l < 9) {
           P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
@@ -579,7 +704,7 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
 #endif
         break;  // scratch is next written two barriers later; bufA/bufB are free
       }
-      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, row0, B);
+      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, ctl, row0, B);
       __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
       if (tid == 0 && P.stamps && step == 0 && l < 10)
@@ -602,6 +727,19 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, con
     P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 3] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
+                                                               float *__restrict__ act, float *__restrict__ hidden,
+                                                               int B, int steps) {
+  fused_body<NW, false>(P, obs, act, hidden, B, steps, nullptr);
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(DevProgram P, DevCtl C, float *__restrict__ hidden,
+                                                                   int B) {
+  fused_body<NW, true>(P, nullptr, nullptr, hidden, B, 1, &C);
 }
 
 // ---------------------------------------------------------------------------
@@ -735,20 +873,26 @@ __device__ __forceinline__ bool sweep_layer(unsigned long long *gran, int n, uns
   }
 }
 
-__global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const DevProgram *__restrict__ Pd,
-                                                                        const float *obs, float *act, int B,
-                                                                        unsigned epoch0, unsigned long long *gran,
-                                                                        int gstride, unsigned *err, unsigned *done) {
-  // the program lives in device memory (uploaded once): a ~60-byte kernarg
-  // instead of the ~700-byte DevProgram keeps the per-launch host cost down
-  const DevProgram &P = *Pd;
+// CTL: controller tick — layer 0 assembles the observation (every workgroup,
+// redundantly: 98 features), the final layer stores through ctl_store, and
+// workgroup 0 (the only one of the one-tile final layer, so every other
+// workgroup's reads of the previous obs / action are done by then) writes the
+// new observation and status before signalling completion.
+template <bool CTL>
+__device__ __forceinline__ void latency_body(const DevProgram &P, const float *obs, float *act, int B,
+                                             unsigned epoch0, unsigned long long *gran, int gstride, unsigned *err,
+                                             unsigned *done, const DevCtl *ctl) {
   extern __shared__ float4 lds4[];
   float *xs = reinterpret_cast<float *>(lds4);               // [B][K_pad] layer input
   float *part = xs + GO2PI_SMALL_MAXB * P.lds_stride;        // [waves][B][16] partial sums
   int &abort_flag = *reinterpret_cast<int *>(part + LAT_WAVES * GO2PI_SMALL_MAXB * 16);  // in the one LDS region
+  // CTL only: raw observation rows [B][in_dim] and per-robot NaN flags
+  float *okeep = part + LAT_WAVES * GO2PI_SMALL_MAXB * 16 + 4;
+  unsigned *nanf = reinterpret_cast<unsigned *>(okeep + GO2PI_SMALL_MAXB * P.in_dim);
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) abort_flag = 0;
+  if (CTL && tid < GO2PI_SMALL_MAXB) nanf[tid] = 0u;
   for (int l = 0; l < P.nl; ++l) {
     const DevLayer &L = P.L[l];
     const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
@@ -764,7 +908,17 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const De
     if (l == 0) {
       for (int e = tid; e < B * K_pad; e += LAT_WAVES * 64) {
         const int b = e / K_pad, k = e - b * K_pad;
-        xs[e] = k < P.in_dim ? prologue(P, obs[(size_t)b * P.in_dim + k], k) : 0.f;
+        float v = 0.f;
+        if (k < P.in_dim) {
+          if constexpr (CTL) {
+            v = ctl_obs_value(*ctl, P.in_dim, b, k);
+            okeep[b * P.in_dim + k] = v;
+          } else {
+            v = obs[(size_t)b * P.in_dim + k];
+          }
+          v = prologue(P, v, k);
+        }
+        xs[e] = v;
       }
     } else if (wave == 0) {
       if (!sweep_layer(gran + (size_t)(l - 1) * gstride, B * K_pad, epoch0 + (unsigned)(l - 1), xs, err, lane))
@@ -810,8 +964,11 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const De
         for (int w2 = 0; w2 < LAT_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
         const float v = act_fn(L.act, L.alpha, s + bv);
         if (last) {
-          if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
-          if (done && b == B - 1 && g == 0) {
+          if (n < L.N) {
+            if constexpr (CTL) ctl_store(*ctl, b, n, post_fn(P, v));
+            else act[(size_t)b * L.N + n] = post_fn(P, v);
+          }
+          if (!CTL && done && b == B - 1 && g == 0) {
             // completion word for the host's spin (instead of a stream sync): every
             // action store of this tile drained and made system-visible first
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -827,6 +984,39 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const De
     }
     __syncthreads();  // xs / part reused by the next layer
   }
+  if constexpr (CTL) {
+    if (g != 0) return;
+    const int H = ctl->prm->hist;
+    for (int e = tid; e < B * P.in_dim; e += LAT_WAVES * 64) {
+      const int b = e / P.in_dim, k = e - b * P.in_dim;
+      const float v = okeep[e];
+      ctl->obs[e] = v;
+      if (__builtin_isnan(v) && ctl_checked(H, k)) atomicOr(nanf + b, 1u);
+    }
+    __syncthreads();
+    if (ctl->status && tid < B) ctl->status[tid] = nanf[tid];
+    // completion word: every store of this workgroup drained and made system-visible first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (done && tid == 0) __hip_atomic_store(done, epoch0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const DevProgram *__restrict__ Pd,
+                                                                        const float *obs, float *act, int B,
+                                                                        unsigned epoch0, unsigned long long *gran,
+                                                                        int gstride, unsigned *err, unsigned *done) {
+  // the program lives in device memory (uploaded once): a ~60-byte kernarg
+  // instead of the ~700-byte DevProgram keeps the per-launch host cost down
+  latency_body<false>(*Pd, obs, act, B, epoch0, gran, gstride, err, done, nullptr);
+}
+
+__global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
+                                                                            int B, unsigned epoch0,
+                                                                            unsigned long long *gran, int gstride,
+                                                                            unsigned *err, unsigned *done) {
+  latency_body<true>(*Pd, nullptr, nullptr, B, epoch0, gran, gstride, err, done, &C);
 }
 
 int latency_grid(const DevProgram &p) {
@@ -849,6 +1039,18 @@ int launch_latency(const DevProgram &p, const DevProgram *p_dev, const float *ob
   return (int)hipGetLastError();
 }
 
+int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, int batch, unsigned epoch0,
+                       unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream) {
+  if (batch <= 0) return 0;
+  if (batch > GO2PI_SMALL_MAXB || p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;
+  const int grid = latency_grid(p);
+  const size_t lds = sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + LAT_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
+                                      (size_t)GO2PI_SMALL_MAXB * p.in_dim + GO2PI_SMALL_MAXB);
+  hipLaunchKernelGGL(policy_latency_ctl_kernel, dim3(grid), dim3(LAT_WAVES * 64), lds,
+                     reinterpret_cast<hipStream_t>(stream), p_dev, ctl, batch, epoch0, gran, gstride, err, done);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 size_t fused_lds_bytes(const DevProgram &p, int waves) {
   // activation buffers + per-wave partial-sum scratch (head fusion: up to 2 tiles)
@@ -862,7 +1064,10 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
 
 template <int NW>
 static hipError_t set_fused_lds(int bytes) {
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
@@ -898,6 +1103,20 @@ int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float 
     default:
       hipLaunchKernelGGL(policy_fused_kernel<8>, grid, dim3(512), lds, s, p, obs, act, hidden, batch, steps);
       break;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, float *hidden, int batch,
+                            void *stream) {
+  if (batch <= 0) return 0;
+  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
+  const size_t lds = fused_lds_bytes(p, waves);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (waves) {
+    case 4: hipLaunchKernelGGL(policy_fused_ctl_kernel<4>, grid, dim3(256), lds, s, p, ctl, hidden, batch); break;
+    case 16: hipLaunchKernelGGL(policy_fused_ctl_kernel<16>, grid, dim3(1024), lds, s, p, ctl, hidden, batch); break;
+    default: hipLaunchKernelGGL(policy_fused_ctl_kernel<8>, grid, dim3(512), lds, s, p, ctl, hidden, batch); break;
   }
   return (int)hipGetLastError();
 }

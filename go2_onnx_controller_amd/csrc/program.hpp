@@ -61,6 +61,39 @@ struct DevProgram {
   DevLayer L[GO2PI_MAX_LAYERS];
 };
 
+// ---------------------------------------------------------------------------
+// Controller tick: the Go2 controller's observation
+// assembly (onnx_controller/src/controller.cpp:173-212, controller.hpp:45-68,
+// 93-110) fused as the policy's prologue and its action post-processing
+// (controller.cpp:217-223, 240-248) fused into the final layer's store.
+// Raw per-robot state row (floats), see include/go2pi.h GO2PI_CTL_*:
+//   [0:4] imu quaternion (w,x,y,z)  [4:7] gyroscope  [7:19] q  [19:31] dq
+//   [31:35] foot_force (Unitree order)  [35] reserved
+// Joystick row: {has_axes, axes[0], axes[1], axes[3], buttons[0]}.
+#define GO2PI_CTL_STATE_DIM 36
+#define GO2PI_CTL_JOY_DIM 5
+#define GO2PI_CTL_DOF 12
+#define GO2PI_CTL_STEP_DIM 49  // kDimObs, controller.hpp:14
+
+struct DevCtlParams {  // device memory, set by go2pi_ctl_set_params
+  double q0[GO2PI_CTL_DOF];
+  double action_scale;
+  double kp_run, kd_run, kp_stop;  // already widened as the reference widens them (float -> double)
+  float action_limit, contact_threshold;
+  float gravity_w[3];
+  int hist;  // kHistory (in_dim / 49)
+};
+
+struct DevCtl {  // per call (kernel argument)
+  const DevCtlParams *prm;
+  const float *state;  // [B][GO2PI_CTL_STATE_DIM]
+  const float *joy;    // [B][GO2PI_CTL_JOY_DIM] or null (no joystick message: vel_cmd kept, buttons[0] = 0)
+  float *obs;          // [B][in_dim]  observation_ with history: read (t-1), written (t)
+  float *action;       // [B][12]      action_: read (t-1, history), written (t)
+  double *q_des, *kp, *kd;  // [B][12] each, or null
+  unsigned *status;         // [B] or null: bit 0 = NaN entered the observation
+};
+
 // Host-side launchers (kernels.hip). All launches are asynchronous on `stream`.
 // Return a hipError_t as int.
 int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float *act, float *hidden, int batch,
@@ -79,5 +112,11 @@ int launch_latency(const DevProgram &p, const DevProgram *p_dev, const float *ob
                    unsigned epoch0,
                    unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream);
 int latency_grid(const DevProgram &p);
+// Controller tick variants of the two launchers above (steps = 1; ctl.obs / ctl.action
+// replace obs / act). The latency variant needs the final layer to be one tile.
+int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, float *hidden, int batch,
+                            void *stream);
+int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, int batch, unsigned epoch0,
+                       unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream);
 
 }  // namespace go2pi

@@ -22,8 +22,14 @@ EXPORTS = [
     "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
     "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
     "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_inspect_model", "go2pi_diag_stamps",
-    "go2pi_last_error", "go2pi_version",
+    "go2pi_last_error", "go2pi_version", "go2pi_ctl_default_params", "go2pi_ctl_set_params",
+    "go2pi_ctl_history", "go2pi_controller_step", "go2pi_controller_step_device",
 ]
+
+# controller tick row layouts (include/go2pi.h GO2PI_CTL_*)
+CTL_STATE_DIM = 36
+CTL_JOY_DIM = 5
+CTL_DOF = 12
 
 GO2PI_OK = 0
 ERRORS = {-1: "GO2PI_E_INVALID", -2: "GO2PI_E_MODEL", -3: "GO2PI_E_DEVICE", -4: "GO2PI_E_CAPACITY"}
@@ -60,6 +66,20 @@ class Cost(ctypes.Structure):
         ("io_bytes_per_row", ctypes.c_double),
         ("n_layers", ctypes.c_int32),
         ("has_gru", ctypes.c_int32),
+    ]
+
+
+class CtlParams(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_int32),
+        ("kp", ctypes.c_float),
+        ("kd", ctypes.c_float),
+        ("kp_stop", ctypes.c_float),
+        ("action_limit", ctypes.c_float),
+        ("contact_threshold", ctypes.c_float),
+        ("gravity_w", ctypes.c_float * 3),
+        ("action_scale", ctypes.c_double),
+        ("q0", ctypes.c_double * 12),
     ]
 
 
@@ -103,6 +123,11 @@ def lib():
             "go2pi_inspect_model": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_last_error": (ctypes.c_char_p, []),
             "go2pi_version": (ctypes.c_char_p, []),
+            "go2pi_ctl_default_params": (None, [P]),
+            "go2pi_ctl_set_params": (ctypes.c_int, [P, P]),
+            "go2pi_ctl_history": (ctypes.c_int, [P, P]),
+            "go2pi_controller_step": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64]),
+            "go2pi_controller_step_device": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -240,6 +265,81 @@ class Engine:
         s = (stream or torch.cuda.current_stream(obs.device)).cuda_stream
         self.run_sequence_device(obs.data_ptr(), out.data_ptr(), T, B, s)
         return out
+
+    # ------------------------------------------------------ controller tick
+    def ctl_history(self):
+        """kHistory of a Go2 controller policy (in_dim / 49); raises otherwise."""
+        h = ctypes.c_int32()
+        _check(lib().go2pi_ctl_history(self._h, ctypes.byref(h)))
+        return h.value
+
+    def ctl_set_params(self, **kw):
+        """Controller parameters (go2pi_ctl_params): kp, kd, kp_stop, action_limit,
+        contact_threshold, gravity_w (3), action_scale, q0 (12). Unnamed ones keep
+        the reference's defaults."""
+        p = CtlParams()
+        lib().go2pi_ctl_default_params(ctypes.byref(p))
+        for k, v in kw.items():
+            if k in ("gravity_w", "q0"):
+                arr = getattr(p, k)
+                if len(v) != len(arr):
+                    raise ValueError(f"{k} needs {len(arr)} values")
+                for i, x in enumerate(v):
+                    arr[i] = float(x)
+            elif hasattr(p, k) and k != "struct_size":
+                setattr(p, k, float(v))
+            else:
+                raise TypeError(f"unknown controller parameter {k!r}")
+        _check(lib().go2pi_ctl_set_params(self._h, ctypes.byref(p)))
+
+    def controller_step(self, state, obs, action, joy=None, outputs=True):
+        """One controller tick on host arrays (go2pi_controller_step).
+        state [B, 36] float32; joy [B, 5] float32 or None; obs [B, in_dim] and
+        action [B, 12] float32 C-contiguous arrays updated IN PLACE (the
+        reference's observation_ / action_). Returns (q_des, kp, kd, status) or
+        None when outputs=False."""
+        st = _f32(state).reshape(-1, CTL_STATE_DIM)
+        B = st.shape[0]
+        for name, a, w in (("obs", obs, self.in_dim), ("action", action, CTL_DOF)):
+            if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous
+                    and a.size == B * w):
+                raise ValueError(f"{name} must be a C-contiguous float32 array of [B, {w}]")
+        jy = None if joy is None else _f32(joy, B * CTL_JOY_DIM)
+        res = None
+        ptrs = [None, None, None, None]
+        if outputs:
+            res = (np.empty((B, CTL_DOF)), np.empty((B, CTL_DOF)), np.empty((B, CTL_DOF)),
+                   np.empty(B, np.uint32))
+            ptrs = [r.ctypes.data for r in res]
+        _check(lib().go2pi_controller_step(self._h, st.ctypes.data, None if jy is None else jy.ctypes.data,
+                                           obs.ctypes.data, action.ctypes.data, *ptrs, B))
+        return res
+
+    def controller_step_device(self, state_ptr, joy_ptr, obs_ptr, action_ptr, q_des_ptr, kp_ptr, kd_ptr,
+                               status_ptr, batch, stream=None):
+        _check(lib().go2pi_controller_step_device(self._h, state_ptr, joy_ptr, obs_ptr, action_ptr, q_des_ptr,
+                                                  kp_ptr, kd_ptr, status_ptr, int(batch), stream))
+
+    def controller_step_torch(self, state, obs, action, joy=None, q_des=None, kp=None, kd=None, status=None,
+                              stream=None):
+        """Device tensors: state [B,36] f32, joy [B,5] f32 or None, obs [B,in] and
+        action [B,12] f32 (updated in place), optional q_des/kp/kd [B,12] float64
+        and status [B] int32 outputs. Enqueued on torch's current stream (or `stream`)."""
+        import torch
+
+        def ptr(t, dtype, width):
+            if t is None:
+                return None
+            if t.dtype != dtype or not t.is_contiguous() or t.device.type != "cuda" or t.numel() != B * width:
+                raise ValueError(f"tensor must be contiguous {dtype} [B, {width}] on the GPU")
+            return t.data_ptr()
+        B = state.shape[0]
+        args = [ptr(state, torch.float32, CTL_STATE_DIM), ptr(joy, torch.float32, CTL_JOY_DIM),
+                ptr(obs, torch.float32, self.in_dim), ptr(action, torch.float32, CTL_DOF),
+                ptr(q_des, torch.float64, CTL_DOF), ptr(kp, torch.float64, CTL_DOF), ptr(kd, torch.float64, CTL_DOF),
+                ptr(status, torch.int32, 1)]
+        s = (stream or torch.cuda.current_stream(state.device)).cuda_stream
+        self.controller_step_device(*args, B, s)
 
     # ------------------------------------------------------ recurrent state
     def reset_hidden(self, mask=None, batch=None):

@@ -125,6 +125,10 @@ MODELS = {
     "gru_small": lambda: gru_model_bytes(I=10, H=32, head=(64, 6), seed=5),
     # launch/sync floor probe (tools/latency_probe.py)
     "tiny": lambda: mlp_model_bytes((4, 16, 4), seed=6),
+    # controller-tick policies (49 * kHistory observations, 12 actions) besides the shipped 98 -> 12
+    "ctl_h1": lambda: mlp_model_bytes((49, 64, 64, 12), seed=7),
+    "ctl_h3": lambda: mlp_model_bytes((147, 128, 128, 12), seed=8),
+    "gru_ctl": lambda: gru_model_bytes(I=98, H=64, head=(128, 12), seed=9),
 }
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -125,6 +125,68 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
    error code; truncates to cap-1 bytes. For loader tests and tooling. */
 int go2pi_inspect_model(const char *onnx_path, char *buf, size_t cap);
 
+/* ---------------------------------------------------------------------------
+   Controller tick: the Go2 ONNXController's per-tick work around act(), fused
+   into the policy launch (many robots or one):
+     prologue  <- observation assembly, controller.cpp:173-212 + lowstate_cb_
+                  controller.hpp:93-110 (gravity projection of the IMU quaternion,
+                  q - q0, joystick velocity command, foot contacts, and the
+                  kHistory-step history shift of populate_buffer, controller.hpp:45-68)
+     epilogue  <- action post-processing, controller.cpp:217-223 (clamp to
+                  +-kActionLimit, joystick stop button zeroes the action) and
+                  240-248 (q_des = q0 + 0.25 a, kp/kd arrays for send_command)
+   Needs a policy whose observation is kHistory x 49 features (kDimObs,
+   controller.hpp:14; the shipped model: 98) and whose action has 12.
+   Per-robot raw state row, GO2PI_CTL_STATE_DIM floats:
+     [0:4]  imu_state.quaternion (w, x, y, z)     [4:7]   imu_state.gyroscope
+     [7:19] joint q (Isaac order)                 [19:31] joint dq
+     [31:35] foot_force (Unitree order, as in LowState)   [35] reserved
+   Per-robot joystick row, GO2PI_CTL_JOY_DIM floats:
+     {has_axes, axes[0], axes[1], axes[3], buttons[0]}; has_axes = 0 keeps the
+     previous velocity command (the reference only updates it when axes are
+     present). A NULL joystick pointer means no message for any robot (velocity
+     command kept, stop button released).
+   State carried between ticks (caller-owned, in place, as the reference's
+   observation_ / action_ members): obs [batch][in_dim] holds the previous
+   observation on entry and this tick's on return (the ObservationAction log
+   row, controller.cpp:226); action [batch][12] holds the previous action on
+   entry and this tick's post-processed action on return. Zero both to start.
+   Outputs q_des / kp / kd [batch][12] (double, as send_command takes them) may
+   be NULL. status [batch] (may be NULL): bit 0 set when a NaN entered the
+   observation (the reference exit(1)s in populate_buffer's check,
+   controller.hpp:57-64); the tick still completes. */
+#define GO2PI_CTL_STATE_DIM 36
+#define GO2PI_CTL_JOY_DIM 5
+#define GO2PI_CTL_DOF 12
+
+typedef struct go2pi_ctl_params {
+  int32_t struct_size;     /* = sizeof(go2pi_ctl_params) */
+  float kp;                /* kp_ (controller.hpp:119), default 28 */
+  float kd;                /* kd_ (:120), default 0.5 */
+  float kp_stop;           /* kp while the stop button is held (controller.cpp:246), default 5 */
+  float action_limit;      /* kActionLimit (controller.hpp:17), default 1000 */
+  float contact_threshold; /* foot_force >= this is a contact (controller.hpp:100-103), default 22 */
+  float gravity_w[3];      /* gravity_w_ (controller.hpp:131), default (0, 0, -1) */
+  double action_scale;     /* q_des = q0 + action_scale * a (controller.cpp:244), default 0.25 */
+  double q0[12];           /* q0_ (controller.hpp:165), Isaac order */
+} go2pi_ctl_params;
+
+void go2pi_ctl_default_params(go2pi_ctl_params *params);
+/* Set the engine's controller parameters (synchronous; defaults at create). */
+int go2pi_ctl_set_params(go2pi_engine *e, const go2pi_ctl_params *params);
+/* kHistory of the bound policy (in_dim / 49), or GO2PI_E_MODEL if its I/O is not
+   a Go2 controller's (in_dim a multiple of 49, out_dim 12). */
+int go2pi_ctl_history(const go2pi_engine *e, int32_t *history);
+
+/* One tick for `batch` robots, host buffers (synchronous; batch <= 8 runs as
+   one launch on host-mapped staging, larger batches stage through HBM). */
+int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy, float *obs, float *action,
+                          double *q_des, double *kp, double *kd, uint32_t *status, int64_t batch);
+/* Same on device pointers, enqueued on `hip_stream`, no host sync. */
+int go2pi_controller_step_device(go2pi_engine *e, const float *state_dev, const float *joy_dev, float *obs_dev,
+                                 float *action_dev, double *q_des_dev, double *kp_dev, double *kd_dev,
+                                 uint32_t *status_dev, int64_t batch, void *hip_stream);
+
 /* Diagnostics: copy up to n per-workgroup clock stamps of the last batched launch
    ({s_memtime, s_memrealtime} at start and end, 4 per workgroup). Needs a
    GO2PI_DIAG_CLOCK build and GO2PI_DIAG_STAMPS set at create; returns the count. */

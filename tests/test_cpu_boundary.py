@@ -143,15 +143,17 @@ def test_create_fails_loudly_without_gpu():
 
 def test_opts_struct_layout_matches_header():
     """ctypes mirror of go2pi_opts / go2pi_cost vs the C compiler's view."""
-    from go2_onnx_controller_amd.engine import Cost, Opts
+    from go2_onnx_controller_amd.engine import Cost, CtlParams, Opts
     src = r'''
 #include <stddef.h>
 #include <stdio.h>
 #include "go2pi.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(go2pi_opts), offsetof(go2pi_opts, obs_mean),
+  printf("%zu %zu %zu %zu %zu %zu ", sizeof(go2pi_opts), offsetof(go2pi_opts, obs_mean),
          offsetof(go2pi_opts, action_scale), sizeof(go2pi_cost), offsetof(go2pi_cost, n_layers),
          offsetof(go2pi_opts, small_batch));
+  printf("%zu %zu %zu %zu\n", sizeof(go2pi_ctl_params), offsetof(go2pi_ctl_params, gravity_w),
+         offsetof(go2pi_ctl_params, action_scale), offsetof(go2pi_ctl_params, q0));
   return 0;
 }'''
     exe = os.path.join(ROOT, "build", "abi_layout")
@@ -160,7 +162,8 @@ int main(void) {
                    check=True)
     got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
     assert got == [ctypes.sizeof(Opts), Opts.obs_mean.offset, Opts.action_scale.offset, ctypes.sizeof(Cost),
-                   Cost.n_layers.offset, Opts.small_batch.offset]
+                   Cost.n_layers.offset, Opts.small_batch.offset, ctypes.sizeof(CtlParams),
+                   CtlParams.gravity_w.offset, CtlParams.action_scale.offset, CtlParams.q0.offset]
 
 
 def build_controller_shape():
