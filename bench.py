@@ -92,6 +92,97 @@ def latency_b1(model_path, device, iters=3000, warm=300):
     return ts[len(ts) // 2], ts[int(len(ts) * 0.99)]
 
 
+def controller_leg(device, steps=200, warm=20, iters=3000):
+    """The fused controller tick (go2pi_controller_step*: observation assembly +
+    shipped policy + action post-processing in one launch):
+    robot-ticks/s at 4096 robots (device path, HIP events on the launch stream)
+    beside the policy-only launch, and the batch-1 host tick p50/p99 (the
+    reference's publish() work around act(), host arrays in and out)."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    from go2_onnx_controller_amd import Engine
+    from go2_onnx_controller_amd.engine import lib
+    path = os.path.join(ROOT, "tests", "golden", "model.onnx")
+    dev = torch.device(f"cuda:{device}")
+    B = 4096
+    g = torch.Generator().manual_seed(3)
+    q0 = torch.tensor([0.1, -0.1, 0.1, -0.1, 0.8, 0.8, 1.0, 1.0, -1.5, -1.5, -1.5, -1.5])
+
+    def states(n):
+        st = torch.zeros((n, 36))
+        quat = torch.cat([torch.ones((n, 1)), 0.08 * torch.randn((n, 3), generator=g)], 1)
+        st[:, 0:4] = quat / quat.norm(dim=1, keepdim=True)
+        st[:, 4:7] = 0.5 * torch.randn((n, 3), generator=g)
+        st[:, 7:19] = q0 + 0.2 * torch.randn((n, 12), generator=g)
+        st[:, 19:31] = 2.0 * torch.randn((n, 12), generator=g)
+        st[:, 31:35] = torch.randint(0, 60, (n, 4), generator=g).float()
+        joy = torch.zeros((n, 5))
+        joy[:, 0] = 1
+        joy[:, 1:4] = torch.rand((n, 3), generator=g) * 2 - 1
+        return st, joy
+    out = {}
+    with Engine(path, device=device, max_batch=B) as e:
+        st, joy = (t.to(dev) for t in states(B))
+        obs = torch.zeros((B, e.in_dim), device=dev)
+        act = torch.zeros((B, 12), device=dev)
+        qd = torch.empty((B, 12), dtype=torch.float64, device=dev)
+        kp, kd = torch.empty_like(qd), torch.empty_like(qd)
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+        s = torch.cuda.Stream(dev)
+        fn = lib().go2pi_controller_step_device
+        P = ctypes.c_void_p
+        args = (e._h, P(st.data_ptr()), P(joy.data_ptr()), P(obs.data_ptr()), P(act.data_ptr()),
+                P(qd.data_ptr()), P(kp.data_ptr()), P(kd.data_ptr()), P(status.data_ptr()), ctypes.c_int64(B),
+                P(s.cuda_stream))
+        policy = e.device_launcher(obs.data_ptr(), act.data_ptr(), B, s.cuda_stream)
+
+        def timed(call):
+            for _ in range(warm):
+                call()
+            torch.cuda.synchronize(dev)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(s)
+            for _ in range(steps):
+                call()
+            ev1.record(s)
+            torch.cuda.synchronize(dev)
+            return ev0.elapsed_time(ev1) / steps * 1e3
+
+        def tick():
+            if fn(*args):
+                raise RuntimeError(lib().go2pi_last_error().decode())
+        tick_us = timed(tick)
+        policy_us = timed(policy)
+        out["robots"] = B
+        out["tick_us"] = round(tick_us, 3)
+        out["policy_only_us"] = round(policy_us, 3)
+        out["robot_ticks_per_s"] = round(B / (tick_us * 1e-6), 1)
+    with Engine(path, device=device, max_batch=8) as e:
+        st1, joy1 = (np.ascontiguousarray(t.numpy()) for t in states(1))
+        obs1 = np.zeros((1, e.in_dim), np.float32)
+        act1 = np.zeros((1, 12), np.float32)
+        bufs = [np.empty((1, 12)), np.empty((1, 12)), np.empty((1, 12)), np.empty(1, np.uint32)]
+        fn = lib().go2pi_controller_step
+        args = (e._h, st1.ctypes.data, joy1.ctypes.data, obs1.ctypes.data, act1.ctypes.data,
+                *[b.ctypes.data for b in bufs], 1)
+        ts = []
+        for i in range(warm * 10 + iters):
+            st1[0, 4 + i % 3] = 0.01 * (i % 7)
+            t0 = time.perf_counter_ns()
+            rc = fn(*args)
+            t1 = time.perf_counter_ns()
+            if rc:
+                raise RuntimeError(lib().go2pi_last_error().decode())
+            if i >= warm * 10:
+                ts.append((t1 - t0) / 1e3)
+        ts.sort()
+        out["b1_tick_p50_us"] = round(ts[len(ts) // 2], 2)
+        out["b1_tick_p99_us"] = round(ts[int(len(ts) * 0.99)], 2)
+    return out
+
+
 def load_pmc(workload, kernel_substr, waves):
     """Memory-side bytes per launch of `kernel_substr` from the committed rocprofv3
     --pmc summary of this workload (tools/profile.sh + tools/summarize_prof.py:
@@ -118,6 +209,7 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency leg")
+    ap.add_argument("--no-ctl", action="store_true", help="skip the controller-tick leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for the barrier / max-time reduce (nccl = RCCL)")
@@ -224,6 +316,8 @@ def main():
             p50, p99 = latency_b1(model_path, local)
             out["latency_b1_p50_us"] = round(p50, 2)
             out["latency_b1_p99_us"] = round(p99, 2)
+        if not args.no_ctl:
+            out["controller_tick"] = controller_leg(local)
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(model_path, in_dim, batch, args.cpu_seconds)
     if rank == 0:

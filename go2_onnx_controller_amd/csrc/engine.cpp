@@ -439,8 +439,14 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     hip_check(hipMemset(p.stamps, 0, e.n_stamps * sizeof(unsigned long long)), "hipMemset");
   }
   // the finished program, copied to device memory for the latency kernel
+  {
+    float *z = e.dalloc<float>(64);
+    hip_check(hipMemset(z, 0, 64 * sizeof(float)), "hipMemset");
+    p.zero = z;
+  }
   // controller tick: a policy with kHistory x 49 observations and 12 actions
-  if (m.in_dim > 0 && m.in_dim % GO2PI_CTL_STEP_DIM == 0 && m.out_dim == GO2PI_CTL_DOF) {
+  if (m.in_dim > 0 && m.in_dim % GO2PI_CTL_STEP_DIM == 0 && m.in_dim <= 16 * GO2PI_CTL_STEP_DIM &&
+      m.out_dim == GO2PI_CTL_DOF) {
     e.ctl_hist = m.in_dim / GO2PI_CTL_STEP_DIM;
     e.d_ctl = e.dalloc<go2pi::DevCtlParams>(1);
     go2pi_ctl_params cp;

@@ -121,15 +121,7 @@ __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
 // copies of a d_b-wide signal, oldest first, and each tick shifts it left by
 // d_b and appends the current value (populate_buffer, controller.hpp:45-52).
 // Blocks: gravity_b 3, base_ang_vel 3, vel_cmd 3, q - q0 12, dq 12, previous
-// action 12, foot contacts 4 (cumulative 0,3,6,9,21,33,45; 49 per step).
-__device__ __forceinline__ void ctl_block(int H, int k, int &b, int &j, int &d) {
-  const int u = k / H;  // position in the 49-wide per-step layout
-  int c;
-  if (u < 9) { b = u / 3; c = 3 * b; d = 3; }
-  else if (u < 45) { b = 3 + (u - 9) / 12; c = 9 + 12 * (b - 3); d = 12; }
-  else { b = 6; c = 45; d = 4; }
-  j = k - H * c;
-}
+// action 12, foot contacts 4 (49 per step).
 
 // gravity_b = quaternion_.inverse() * gravity_w_ (controller.cpp:182-184) with
 // Eigen 3.4 semantics: inverse() = conjugate / squaredNorm (the zero quaternion
@@ -137,7 +129,7 @@ __device__ __forceinline__ void ctl_block(int H, int k, int &b, int &j, int &d) 
 // the (x,y,z,w) coefficients), and q * v = _transformVector:
 // uv = 2 (q.vec × v), r = (v + w uv) + q.vec × uv. Every operation rounds to
 // fp32 in that order (no fma contraction), like the reference's x86 build.
-__device__ __forceinline__ float ctl_gravity(const float *st, const float *gw, int i) {
+__device__ __forceinline__ float ctl_gravity(const float *st, float v0, float v1, float v2, int i) {
 #pragma clang fp contract(off)
   const float w = st[0], x = st[1], y = st[2], z = st[3];
   const float n2 = (x * x + z * z) + (y * y + w * w);
@@ -148,7 +140,6 @@ __device__ __forceinline__ float ctl_gravity(const float *st, const float *gw, i
     qz = -z / n2;
     qw = w / n2;
   }
-  const float v0 = gw[0], v1 = gw[1], v2 = gw[2];
   float u0 = qy * v2 - qz * v1, u1 = qz * v0 - qx * v2, u2 = qx * v1 - qy * v0;
   u0 += u0;
   u1 += u1;
@@ -159,57 +150,188 @@ __device__ __forceinline__ float ctl_gravity(const float *st, const float *gw, i
   return (v2 + qw * u2) + c2;
 }
 
-// Raw (un-normalised) observation feature k of robot `row` for this tick.
-// Reads the previous tick's observation (history) and action; obs is updated
-// in place by the caller only after every read of the tile is done.
-__device__ __forceinline__ float ctl_obs_value(const DevCtl &C, int in_dim, int row, int k) {
-  const DevCtlParams &Q = *C.prm;
-  const int H = Q.hist;
-  int b, j, d;
-  ctl_block(H, k, b, j, d);
-  const float *orow = C.obs + (size_t)row * in_dim;
-  if (j < (H - 1) * d) return orow[k + d];  // shifted history
-  const int i = j - (H - 1) * d;
-  const float *st = C.state + (size_t)row * GO2PI_CTL_STATE_DIM;
-  switch (b) {
-    case 0: return ctl_gravity(st, Q.gravity_w, i);
-    case 1: return st[4 + i];  // imu gyroscope (controller.hpp:105-109)
-    case 2: {                  // vel_cmd from the joystick (controller.cpp:173-179), sticky without one
-      const float *jy = C.joy ? C.joy + (size_t)row * GO2PI_CTL_JOY_DIM : nullptr;
-      if (!jy || jy[0] == 0.f) return orow[k];  // previous tick's vel_cmd_
-      if (i == 0) return jy[2];                 // axes[1]
-      if (i == 2) return jy[3] * jy[2];         // axes[3] * axes[1]
-      const double a0 = jy[1];                  // pow(axes[0], 2) * sign * 0.8, in double
-      return (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
-    }
-    case 3: return (float)((double)st[7 + i] - Q.q0[i]);  // q_[i] -= q0_[i] (double q0_)
-    case 4: return st[19 + i];
-    case 5: return C.action[(size_t)row * GO2PI_CTL_DOF + i];  // action_ before act()
-    default:  // contacts: foot_force >= 22 with the FR/FL, RR/RL swap (controller.hpp:99-103)
-      return st[31 + (i ^ 1)] >= Q.contact_threshold ? 1.f : 0.f;
+// Direct-to-LDS copy of n contiguous floats (global_load_lds_dword: no VGPR
+// round trip, every load of the workgroup in flight at once). dst needs room
+// for ceil64(n) floats (the tail lanes re-read element n-1). Complete after
+// the next __syncthreads() (its fence waits vmcnt(0)).
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ void glds_copy(float *dst, const float *src, int n, int wave, int lane, int nw) {
+  for (int base = wave * 64; base < n; base += nw * 64) {
+    const int i = min(base + lane, n - 1);
+    __builtin_amdgcn_global_load_lds((gvoid_t *)(src + i), (lvoid_t *)(dst + base), 4, 0, 0);
   }
 }
 
-// Features the reference checks after each single-signal populate_buffer: a
-// NaN there makes it exit(1) (controller.hpp:57-64); flagged in status here.
-__device__ __forceinline__ bool ctl_checked(int H, int k) {
-  int b, j, d;
-  ctl_block(H, k, b, j, d);
-  return b < 6 && j >= (H - 1) * d;
+// LDS image of one tile's controller inputs (rows r < R of the tile): q0
+// (double), raw state rows, joystick rows, previous action / observation rows,
+// per-row NaN flags. Plain values passed by value (no address-taken locals:
+// nothing spills to scratch).
+struct CtlLds {
+  double *q0;
+  float *st, *jy, *act, *obs;
+  unsigned *nanf;
+};
+
+__host__ __device__ inline int ctl_lds_floats(int R, int in_dim) {
+  auto c64 = [](int x) { return (x + 63) & ~63; };
+  return 24 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) + c64(R * in_dim) +
+         GO2PI_TILE_ROWS;
+}
+
+__device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim) {
+  auto c64 = [](int x) { return (x + 63) & ~63; };
+  CtlLds L;
+  L.q0 = reinterpret_cast<double *>(base);
+  L.st = base + 24;
+  L.jy = L.st + c64(R * GO2PI_CTL_STATE_DIM);
+  L.act = L.jy + c64(R * GO2PI_CTL_JOY_DIM);
+  L.obs = L.act + c64(R * GO2PI_CTL_DOF);
+  L.nanf = reinterpret_cast<unsigned *>(L.obs + c64(R * in_dim));
+  return L;
+}
+
+// Issue the direct-to-LDS loads of rows [row0, row0 + nrows) and clear the NaN flags.
+__device__ __forceinline__ void ctl_lds_load(const CtlLds L, const DevCtl C, int row0, int nrows, int in_dim, int tid,
+                                             int wave, int lane, int nw) {
+  glds_copy(L.st, C.state + (size_t)row0 * GO2PI_CTL_STATE_DIM, nrows * GO2PI_CTL_STATE_DIM, wave, lane, nw);
+  if (C.joy) glds_copy(L.jy, C.joy + (size_t)row0 * GO2PI_CTL_JOY_DIM, nrows * GO2PI_CTL_JOY_DIM, wave, lane, nw);
+  glds_copy(L.act, C.action + (size_t)row0 * GO2PI_CTL_DOF, nrows * GO2PI_CTL_DOF, wave, lane, nw);
+  glds_copy(L.obs, C.obs + (size_t)row0 * in_dim, nrows * in_dim, wave, lane, nw);
+  if (tid < GO2PI_CTL_DOF) L.q0[tid] = C.prm->q0[tid];
+  if (tid < GO2PI_TILE_ROWS) L.nanf[tid] = 0u;
+}
+
+// Controller parameters the assembly reads, loaded once at kernel start (by
+// value: their scalar loads overlap the input staging instead of following it).
+struct CtlQ {
+  int hist;
+  float thr, g0, g1, g2;
+};
+
+__device__ __forceinline__ CtlQ ctl_q(const DevCtl C) {
+  const DevCtlParams &Q = *C.prm;
+  return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2]};
+}
+
+// One history block BK of the new observation rows r < nrows, on one wave's
+// lanes: straight-line code per block (BK is a template parameter).
+template <int BK, bool TILE>
+__device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
+                                               float *dst, int ds, float *raw, int lane) {
+  constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
+  constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
+  const int H = q.hist, in_dim = P.in_dim;
+  const int W = H * d, s0 = H * cum, sh = (H - 1) * d;
+  const float rW = 1.f / (float)W;
+#pragma unroll 2
+  for (int e = lane; e < nrows * W; e += 64) {
+    // r = e / W exactly: (e + 0.5) / W is >= 0.5 / W away from an integer and the
+    // float product's error is far below that for these sizes (W <= 49 * 16)
+    const int r = (int)(((float)e + 0.5f) * rW);
+    const int j = e - r * W, k = s0 + j;
+    const float *orow = L.obs + r * in_dim;
+    float v;
+    if (j < sh) {
+      v = orow[k + d];  // std::shift_left by d
+    } else {
+      const int i = j - sh;
+      const float *st = L.st + r * GO2PI_CTL_STATE_DIM;
+      if constexpr (BK == 0) {
+        v = ctl_gravity(st, q.g0, q.g1, q.g2, i);
+      } else if constexpr (BK == 1) {
+        v = st[4 + i];  // imu gyroscope (controller.hpp:105-109)
+      } else if constexpr (BK == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
+        const float *jy = L.jy + r * GO2PI_CTL_JOY_DIM;
+        if (!joy || jy[0] == 0.f) v = orow[k];  // the previous tick's vel_cmd_
+        else if (i == 0) v = jy[2];             // axes[1]
+        else if (i == 2) v = jy[3] * jy[2];     // axes[3] * axes[1]
+        else {                                  // pow(axes[0], 2) * sign * 0.8 in double
+          const double a0 = jy[1];
+          v = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
+        }
+      } else if constexpr (BK == 3) {
+        v = (float)((double)st[7 + i] - L.q0[i]);  // q_[i] -= q0_[i] (double q0_)
+      } else if constexpr (BK == 4) {
+        v = st[19 + i];
+      } else if constexpr (BK == 5) {
+        v = L.act[r * GO2PI_CTL_DOF + i];  // action_ before act()
+      } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
+        v = st[31 + (i ^ 1)] >= q.thr ? 1.f : 0.f;
+      }
+      if (BK < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
+    }
+    if (raw) raw[r * in_dim + k] = v;
+    dst[r * ds + k] = TILE ? prologue(P, v, k) : v;
+  }
+}
+
+// Assemble this tick's observation rows r < nrows from the LDS image: one job
+// per history block spread over the waves (each wave runs one block's
+// straight-line code), plus — TILE: dst is the batched kernel's LDS tile — a
+// job zeroing its padding columns [in_dim, in_pad) and rows [nrows, 16).
+// Per element: the raw value goes to raw[r * in_dim + k] (the tile's global
+// obs rows; may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k].
+// NaN among the appended values of blocks 0-5 — where the reference's
+// populate_buffer check exit(1)s (controller.hpp:57-64) — sets nanf[r].
+// Needs the image complete (barrier).
+template <bool TILE>
+__device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
+                                             float *dst, int ds, float *raw, int wave, int lane, int nw) {
+  for (int job = wave; job < 8; job += nw) {
+    switch (job) {
+      case 0: ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 1: ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 2: ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 3: ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 4: ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 5: ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      case 6: ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
+      default:
+        if constexpr (TILE) {  // padding
+          const int in_dim = P.in_dim, pw = P.in_pad - in_dim;
+          const float rp = 1.f / (float)pw;
+          for (int e = lane; e < nrows * pw; e += 64) {
+            const int r = (int)(((float)e + 0.5f) * rp);
+            dst[r * ds + in_dim + (e - r * pw)] = 0.f;
+          }
+          for (int r = nrows; r < GO2PI_TILE_ROWS; ++r)
+            for (int k = lane; k < P.in_pad; k += 64) dst[r * ds + k] = 0.f;
+        }
+        break;
+    }
+  }
+}
+
+// What the final layer's store needs (controller tick), by value: the call's
+// output pointers, the parameters, and this tile's LDS q0 / joystick rows.
+struct CtlView {
+  float *action;
+  double *q_des, *kp, *kd;
+  const double *q0;
+  const float *jy;  // null: no joystick
+  double scale, kp_run, kp_stop, kd_run;
+  float lim;
+  int row0;
+  int on;  // 0: plain policy launch (the final layer writes `out`)
+};
+
+__device__ __forceinline__ CtlView ctl_view(const DevCtl C, const CtlLds L, int row0) {
+  const DevCtlParams &Q = *C.prm;
+  return CtlView{C.action, C.q_des, C.kp, C.kd, L.q0, C.joy ? L.jy : nullptr, Q.action_scale, Q.kp_run,
+                 Q.kp_stop, Q.kd_run, Q.action_limit, row0, 1};
 }
 
 // Action post-processing of robot `row`, joint n (controller.cpp:217-223, 240-248).
-__device__ __forceinline__ void ctl_store(const DevCtl &C, int row, int n, float v) {
-  const DevCtlParams &Q = *C.prm;
-  const float lim = Q.action_limit;
-  float a = v < -lim ? -lim : (lim < v ? lim : v);  // std::clamp (NaN passes through)
-  const bool stop = C.joy && C.joy[(size_t)row * GO2PI_CTL_JOY_DIM + 4] != 0.f;
+__device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float v) {
+  float a = v < -V.lim ? -V.lim : (V.lim < v ? V.lim : v);  // std::clamp (NaN passes through)
+  const bool stop = V.jy && V.jy[(row - V.row0) * GO2PI_CTL_JOY_DIM + 4] != 0.f;
   a *= stop ? 0.f : 1.f;  // a *= joy_->buttons[0] == 0
   const size_t o = (size_t)row * GO2PI_CTL_DOF + n;
-  C.action[o] = a;
-  if (C.q_des) C.q_des[o] = Q.q0[n] + (double)a * Q.action_scale;
-  if (C.kp) C.kp[o] = stop ? Q.kp_stop : Q.kp_run;
-  if (C.kd) C.kd[o] = Q.kd_run;
+  V.action[o] = a;
+  if (V.q_des) V.q_des[o] = V.q0[n] + (double)a * V.scale;
+  if (V.kp) V.kp[o] = stop ? V.kp_stop : V.kp_run;
+  if (V.kd) V.kd[o] = V.kd_run;
 }
 
 // ---------------------------------------------------------------------------
@@ -255,7 +377,8 @@ __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, c
   // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
   // a trailing load would only be waited for by the epilogue
   // (A operands are read per 4-chunk group; double-buffering them across groups
-  // measured slower: 100.4K vs 97.8K cycles per workgroup)
+  // measured slower: 100.4K vs 97.8K cycles per workgroup; fragments 2 chunks
+  // ahead instead of 1 measured slower too: 98.1K vs 96.2K)
   auto group = [&](int c, auto tail_k) {
     constexpr bool TAIL = decltype(tail_k)::value;
     float4 a[4];
@@ -303,7 +426,7 @@ __device__ __forceinline__ void load_bias(float (&bv)[TPW], const float *__restr
 template <int TPW>
 __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW],
                                             const float (&bv)[TPW], int t_first, int T, int lane, bool last, float *Y,
-                                            int ys, float *out, const DevCtl *ctl, int row0, int B) {
+                                            int ys, float *out, const CtlView ctl, int row0, int B) {
   const int col = lane & 15, r0 = (lane >> 4) << 2;
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
@@ -322,7 +445,7 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
           const int row = row0 + r0 + r;
           if (row >= B) continue;
           const float v = post_fn(P, act_t<ACT>(alpha, acc[i][r] + bv[i]));
-          if (ctl) ctl_store(*ctl, row, n, v);  // controller tick: action post-processing
+          if (ctl.on) ctl_store(ctl, row, n, v);  // controller tick: action post-processing
           else out[(size_t)row * L.N + n] = v;
         }
       }
@@ -338,7 +461,7 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
 template <int TPW, int HT>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out,
-                                            const DevCtl *ctl, int row0, int B, const DevLayer *HL,
+                                            const CtlView ctl, int row0, int B, const DevLayer *HL,
                                             f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   constexpr int HN = HT > 0 ? HT : 1;
   f32x4 acc[TPW];
@@ -392,7 +515,7 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 template <int TPW>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out,
-                                            const DevCtl *ctl, int row0, int B) {
+                                            const CtlView ctl, int row0, int B) {
   f32x4 none[1];
   dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none);
 }
@@ -401,7 +524,7 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 // with the fused head (HT > 0). Barrier-free.
 template <int NW, int HT>
 __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int wave, int lane, bool last, float *out, const DevCtl *ctl, int row0,
+                                            int wave, int lane, bool last, float *out, const CtlView ctl, int row0,
                                             int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   // largest tile group per pass: bounded so the accumulators fit the VGPR
@@ -432,14 +555,14 @@ __device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevL
   f32x4 hacc[HT];
 #pragma unroll
   for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, nullptr, row0, B, &HL, hacc);
+  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc);
 #pragma unroll
   for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
 }
 
 template <int NW>
 __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer &HL, const f32x4 *scratch, int wave,
-                                            int lane, float *out, const DevCtl *ctl, int row0, int B) {
+                                            int lane, float *out, const CtlView ctl, int row0, int B) {
   const int T = HL.N_pad >> 4;
   if (wave >= T) return;
   f32x4 acc[1] = {scratch[(wave * NW) * 64 + lane]};
@@ -454,7 +577,7 @@ __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer 
 template <int NW>
 __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             f32x4 *scratch, int wave, int lane, bool last, float *out,
-                                            const DevCtl *ctl, int row0, int B) {
+                                            const CtlView ctl, int row0, int B) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
     f32x4 none[1];
@@ -583,12 +706,12 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
 }
 
 // Body of the batched kernel. CTL: controller tick (steps == 1) — the
-// observation is assembled from raw robot state (ctl_obs_value) instead of
+// observation is assembled from raw robot state (ctl_assemble) instead of
 // read, and the final layer's store is the action post-processing (ctl_store).
 template <int NW, bool CTL>
 __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
                                            float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
-                                           const DevCtl *ctl) {
+                                           const DevCtl ctl) {
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   const int S = P.lds_stride;
@@ -616,20 +739,46 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   }
 #endif
 
+  // controller tick: this tile's raw inputs staged in LDS behind the scratch
+  // region (one burst of direct-to-LDS loads), then assembled from there
+  const CtlLds CL = ctl_lds(lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S + 256 * NW * (P.head_fuse > 1 ? P.head_fuse : 1),
+                            GO2PI_TILE_ROWS, P.in_dim);
+  CtlView cv{};
+  CtlQ cq{};
+  if constexpr (CTL) {
+    cq = ctl_q(ctl);
+    cv = ctl_view(ctl, CL, row0);
+    ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
+    __syncthreads();
+#ifdef GO2PI_DIAG_CLOCK
+    if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 5] = __builtin_amdgcn_s_memtime();
+#endif
+  }
+  // plain observation rows with no prologue arithmetic are staged by direct-to-LDS
+  // loads (needs whole 64-column chunks to fit the LDS row)
+  const bool glds_obs = !CTL && !P.pre_sub && !P.pre_div && !(P.obs_clip > 0.f) && ((P.in_pad + 63) & ~63) <= S;
   auto stage_obs = [&](int step) {
-    const float *ob = obs + (size_t)step * B * P.in_dim;
-    for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
-      const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
-      float v = 0.f;
-      if constexpr (CTL) {  // raw value; written back to ctl->obs and normalised after the barrier
-        if (row < B && k < P.in_dim) {
-          v = ctl_obs_value(*ctl, P.in_dim, row, k);
-          if (k == 0 && ctl->status) ctl->status[row] = 0u;
-        }
-      } else {
-        if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
+    if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
+      ctl_assemble<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
+                         ctl.obs + (size_t)row0 * P.in_dim, wave, lane, NW);
+    } else if (glds_obs) {
+      // one direct-to-LDS load per (row, 64-column chunk): the tile's observation
+      // loads all in flight together; padding lanes and rows past B read zeros
+      const float *ob = obs + (size_t)step * B * P.in_dim;
+      const int nch = (P.in_pad + 63) >> 6;
+      for (int jb = wave; jb < GO2PI_TILE_ROWS * nch; jb += NW) {
+        const int r = jb / nch, c = jb - r * nch, row = row0 + r, k = c * 64 + lane;
+        const float *src = (row < B && k < P.in_dim) ? ob + (size_t)row * P.in_dim + k : P.zero + lane;
+        __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
       }
-      bufA[r * S + k] = v;
+    } else {
+      const float *ob = obs + (size_t)step * B * P.in_dim;
+      for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
+        const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
+        float v = 0.f;
+        if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
+        bufA[r * S + k] = v;
+      }
     }
   };
   // Step 0's observation loads go out first; their HBM latency overlaps the
@@ -659,23 +808,15 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     float *ac = act + (size_t)step * B * P.out_dim;
     if (step > 0) stage_obs(step);
     __syncthreads();
-    if constexpr (CTL) {
-      // every read of this tile's previous obs / action happened before the barrier:
-      // publish the new observation (the ObservationAction log, controller.cpp:226)
-      const bool norm = P.pre_sub || P.pre_div || P.obs_clip > 0.f;
-      for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
-        const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
-        if (row >= B || k >= P.in_dim) continue;
-        const float v = bufA[r * S + k];
-        ctl->obs[(size_t)row * P.in_dim + k] = v;
-        if (ctl->status && __builtin_isnan(v) && ctl_checked(ctl->prm->hist, k)) atomicOr(ctl->status + row, 1u);
-        if (norm) bufA[r * S + k] = prologue(P, v, k);
-      }
-      if (norm) __syncthreads();
-    }
 #ifdef GO2PI_DIAG_CLOCK
     if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
+    if constexpr (CTL) {
+      if (ctl.status && tid < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + tid] = CL.nanf[tid];
+#ifdef GO2PI_DIAG_CLOCK
+      if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
+#endif
+    }
     float *X = bufA, *Y = bufB;
     if (P.has_gru) {
       gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
@@ -695,7 +836,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         if (P.head_fuse == 1) dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
         else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
         __syncthreads();
-        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, ctl, row0, B);
+        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, cv, row0, B);
 #ifdef GO2PI_DIAG_CLOCK
         if (tid == 0 && P.stamps && step == 0 && l < 9) {
           P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
@@ -704,7 +845,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 #endif
         break;  // scratch is next written two barriers later; bufA/bufB are free
       }
-      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, ctl, row0, B);
+      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B);
       __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
       if (tid == 0 && P.stamps && step == 0 && l < 10)
@@ -733,13 +874,13 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
                                                                float *__restrict__ act, float *__restrict__ hidden,
                                                                int B, int steps) {
-  fused_body<NW, false>(P, obs, act, hidden, B, steps, nullptr);
+  fused_body<NW, false>(P, obs, act, hidden, B, steps, DevCtl{});
 }
 
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(DevProgram P, DevCtl C, float *__restrict__ hidden,
                                                                    int B) {
-  fused_body<NW, true>(P, nullptr, nullptr, hidden, B, 1, &C);
+  fused_body<NW, true>(P, nullptr, nullptr, hidden, B, 1, C);
 }
 
 // ---------------------------------------------------------------------------
@@ -881,18 +1022,24 @@ __device__ __forceinline__ bool sweep_layer(unsigned long long *gran, int n, uns
 template <bool CTL>
 __device__ __forceinline__ void latency_body(const DevProgram &P, const float *obs, float *act, int B,
                                              unsigned epoch0, unsigned long long *gran, int gstride, unsigned *err,
-                                             unsigned *done, const DevCtl *ctl) {
+                                             unsigned *done, const DevCtl ctl) {
   extern __shared__ float4 lds4[];
   float *xs = reinterpret_cast<float *>(lds4);               // [B][K_pad] layer input
   float *part = xs + GO2PI_SMALL_MAXB * P.lds_stride;        // [waves][B][16] partial sums
   int &abort_flag = *reinterpret_cast<int *>(part + LAT_WAVES * GO2PI_SMALL_MAXB * 16);  // in the one LDS region
-  // CTL only: raw observation rows [B][in_dim] and per-robot NaN flags
+  // CTL only: the new raw observation rows [B][in_dim], then the LDS image of the inputs
   float *okeep = part + LAT_WAVES * GO2PI_SMALL_MAXB * 16 + 4;
-  unsigned *nanf = reinterpret_cast<unsigned *>(okeep + GO2PI_SMALL_MAXB * P.in_dim);
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) abort_flag = 0;
-  if (CTL && tid < GO2PI_SMALL_MAXB) nanf[tid] = 0u;
+  const CtlLds CL = ctl_lds(okeep + GO2PI_SMALL_MAXB * P.in_dim, GO2PI_SMALL_MAXB, P.in_dim);
+  CtlView cv{};
+  CtlQ cq{};
+  if constexpr (CTL) {
+    cq = ctl_q(ctl);
+    cv = ctl_view(ctl, CL, 0);
+    if (g < (P.L[0].N_pad >> 4)) ctl_lds_load(CL, ctl, 0, B, P.in_dim, tid, wave, lane, LAT_WAVES);  // layer-0 WGs
+  }
   for (int l = 0; l < P.nl; ++l) {
     const DevLayer &L = P.L[l];
     const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
@@ -906,19 +1053,16 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
     }
     const float bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
     if (l == 0) {
+      const float *src = obs;
+      if constexpr (CTL) {
+        __syncthreads();  // the LDS image of the inputs (and the weights above) landed
+        ctl_assemble<false>(P, CL, cq, ctl.joy != nullptr, B, okeep, P.in_dim, nullptr, wave, lane, LAT_WAVES);
+        __syncthreads();
+        src = okeep;
+      }
       for (int e = tid; e < B * K_pad; e += LAT_WAVES * 64) {
         const int b = e / K_pad, k = e - b * K_pad;
-        float v = 0.f;
-        if (k < P.in_dim) {
-          if constexpr (CTL) {
-            v = ctl_obs_value(*ctl, P.in_dim, b, k);
-            okeep[b * P.in_dim + k] = v;
-          } else {
-            v = obs[(size_t)b * P.in_dim + k];
-          }
-          v = prologue(P, v, k);
-        }
-        xs[e] = v;
+        xs[e] = k < P.in_dim ? prologue(P, src[(size_t)b * P.in_dim + k], k) : 0.f;
       }
     } else if (wave == 0) {
       if (!sweep_layer(gran + (size_t)(l - 1) * gstride, B * K_pad, epoch0 + (unsigned)(l - 1), xs, err, lane))
@@ -965,7 +1109,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
         const float v = act_fn(L.act, L.alpha, s + bv);
         if (last) {
           if (n < L.N) {
-            if constexpr (CTL) ctl_store(*ctl, b, n, post_fn(P, v));
+            if constexpr (CTL) ctl_store(cv, b, n, post_fn(P, v));
             else act[(size_t)b * L.N + n] = post_fn(P, v);
           }
           if (!CTL && done && b == B - 1 && g == 0) {
@@ -986,15 +1130,8 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
   }
   if constexpr (CTL) {
     if (g != 0) return;
-    const int H = ctl->prm->hist;
-    for (int e = tid; e < B * P.in_dim; e += LAT_WAVES * 64) {
-      const int b = e / P.in_dim, k = e - b * P.in_dim;
-      const float v = okeep[e];
-      ctl->obs[e] = v;
-      if (__builtin_isnan(v) && ctl_checked(H, k)) atomicOr(nanf + b, 1u);
-    }
-    __syncthreads();
-    if (ctl->status && tid < B) ctl->status[tid] = nanf[tid];
+    for (int e = tid; e < B * P.in_dim; e += LAT_WAVES * 64) ctl.obs[e] = okeep[e];
+    if (ctl.status && tid < B) ctl.status[tid] = CL.nanf[tid];
     // completion word: every store of this workgroup drained and made system-visible first
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1009,14 +1146,14 @@ __global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_kernel(const De
                                                                         int gstride, unsigned *err, unsigned *done) {
   // the program lives in device memory (uploaded once): a ~60-byte kernarg
   // instead of the ~700-byte DevProgram keeps the per-launch host cost down
-  latency_body<false>(*Pd, obs, act, B, epoch0, gran, gstride, err, done, nullptr);
+  latency_body<false>(*Pd, obs, act, B, epoch0, gran, gstride, err, done, DevCtl{});
 }
 
 __global__ __launch_bounds__(LAT_WAVES * 64) void policy_latency_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
                                                                             int B, unsigned epoch0,
                                                                             unsigned long long *gran, int gstride,
                                                                             unsigned *err, unsigned *done) {
-  latency_body<true>(*Pd, nullptr, nullptr, B, epoch0, gran, gstride, err, done, &C);
+  latency_body<true>(*Pd, nullptr, nullptr, B, epoch0, gran, gstride, err, done, C);
 }
 
 int latency_grid(const DevProgram &p) {
@@ -1045,7 +1182,8 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
   if (batch > GO2PI_SMALL_MAXB || p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;
   const int grid = latency_grid(p);
   const size_t lds = sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + LAT_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
-                                      (size_t)GO2PI_SMALL_MAXB * p.in_dim + GO2PI_SMALL_MAXB);
+                                      (size_t)GO2PI_SMALL_MAXB * p.in_dim + GO2PI_SMALL_MAXB +
+                                      ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim));
   hipLaunchKernelGGL(policy_latency_ctl_kernel, dim3(grid), dim3(LAT_WAVES * 64), lds,
                      reinterpret_cast<hipStream_t>(stream), p_dev, ctl, batch, epoch0, gran, gstride, err, done);
   return (int)hipGetLastError();
@@ -1062,22 +1200,27 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
   return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
 }
 
+static size_t fused_ctl_lds_bytes(const DevProgram &p, int waves) {
+  return fused_lds_bytes(p, waves) + sizeof(float) * ctl_lds_floats(GO2PI_TILE_ROWS, p.in_dim);
+}
+
 template <int NW>
-static hipError_t set_fused_lds(int bytes) {
+static hipError_t set_fused_lds(const DevProgram &p) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds_bytes(p, NW));
   if (e != hipSuccess) return e;
+  const size_t ctl = fused_ctl_lds_bytes(p, NW);
+  if (ctl > 160 * 1024) return hipSuccess;  // controller tick unavailable for this width (launch fails loudly)
   return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)ctl);
 }
 
 int configure_kernels(const DevProgram &p, int waves) {
   hipError_t e = hipSuccess;
-  const int bytes = (int)fused_lds_bytes(p, waves);
   switch (waves) {
-    case 4: e = set_fused_lds<4>(bytes); break;
-    case 16: e = set_fused_lds<16>(bytes); break;
-    default: e = set_fused_lds<8>(bytes); break;
+    case 4: e = set_fused_lds<4>(p); break;
+    case 16: e = set_fused_lds<16>(p); break;
+    default: e = set_fused_lds<8>(p); break;
   }
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
@@ -1111,7 +1254,8 @@ int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, f
                             void *stream) {
   if (batch <= 0) return 0;
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
-  const size_t lds = fused_lds_bytes(p, waves);
+  const size_t lds = fused_ctl_lds_bytes(p, waves);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (waves) {
     case 4: hipLaunchKernelGGL(policy_fused_ctl_kernel<4>, grid, dim3(256), lds, s, p, ctl, hidden, batch); break;

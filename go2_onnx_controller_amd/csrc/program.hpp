@@ -58,6 +58,7 @@ struct DevProgram {
   float clip_lo, clip_hi, scale;
   DevGru gru;
   unsigned long long *stamps;  // diagnostics only (GO2PI_DIAG_CLOCK builds): 4 per workgroup
+  const float *zero;           // >= 64 zero floats in device memory (source of the padding lanes' loads)
   DevLayer L[GO2PI_MAX_LAYERS];
 };
 

@@ -22,22 +22,42 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--model", default="go2_mlp_512")
+    ap.add_argument("--ctl", action="store_true", help="time the controller tick (shipped-layout policy)")
     args = ap.parse_args()
     os.environ.setdefault("GO2PI_DIAG_STAMPS", "1")
     import numpy as np
     import torch
     from go2_onnx_controller_amd import Engine, synth
-    e = Engine(synth.ensure_model(args.model), max_batch=args.batch, waves=args.waves)
+    path = args.model if args.model.endswith(".onnx") else synth.ensure_model(args.model)
+    e = Engine(path, max_batch=args.batch, waves=args.waves)
     x = torch.randn(args.batch, e.in_dim, device="cuda:0")
     y = torch.empty(args.batch, e.out_dim, device="cuda:0")
     s = torch.cuda.Stream()
+    if args.ctl:
+        st = torch.zeros(args.batch, 36, device="cuda:0")
+        st[:, 0] = 1
+        joy = torch.zeros(args.batch, 5, device="cuda:0")
+        q = torch.empty(args.batch, 12, dtype=torch.float64, device="cuda:0")
+        kp, kd = torch.empty_like(q), torch.empty_like(q)
+        status = torch.empty(args.batch, dtype=torch.int32, device="cuda:0")
+
+        def call():
+            e.controller_step_torch(st, x, y, joy=joy, q_des=q, kp=kp, kd=kd, status=status, stream=s)
+    else:
+        def call():
+            e.run_torch(x, out=y, stream=s)
     t0 = time.time()
     n = 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    per_launch = []
     while time.time() - t0 < args.seconds:
+        ev0.record(s)
         for _ in range(50):
-            e.run_torch(x, out=y, stream=s)
+            call()
+        ev1.record(s)
         n += 50
         s.synchronize()
+        per_launch.append(ev0.elapsed_time(ev1) * 1e3 / 50)
     SPW = 64
     st = e.diag_stamps(SPW * ((args.batch + 15) // 16)).reshape(-1, SPW).astype(np.float64)
     nl = e.cost["n_layers"]
@@ -48,8 +68,12 @@ def main():
         if np.all(s0 > 0):
             waves_l1[w] = [float(np.median(s0 - st[:, 6])), float(np.median(s1 - st[:, 6])),
                            float(np.median(s2 - st[:, 6])), float(np.median(st[:, 7] - st[:, 6]))]
-    marks = [st[:, 0], st[:, 4]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
-    names = ["init"] + [f"layer{l}" for l in range(nl)] + ["tail"]
+    if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
+        marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
+        names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
+    else:
+        marks = [st[:, 0], st[:, 4]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
+        names = ["init"] + [f"layer{l}" for l in range(nl)] + ["tail"]
     phases = {n: float(np.median(b - a)) for n, a, b in zip(names, marks[:-1], marks[1:])}
     cyc = st[:, 2] - st[:, 0]
     rt = (st[:, 3] - st[:, 1]) / 100e6
@@ -59,6 +83,9 @@ def main():
            "clock_ghz_min": float(clk.min() / 1e9), "wg_cycles_median": float(np.median(cyc)),
            "wg_us_median": float(np.median(rt) * 1e6), "wg_us_max": float(rt.max() * 1e6),
            "launch_span_us": float((st[:, 3].max() - st[:, 1].min()) / 100),
+           "event_us_per_launch": float(np.median(per_launch)),
+           "wg_start_spread_us": float((st[:, 1].max() - st[:, 1].min()) / 100),
+           "wg_end_spread_us": float((st[:, 3].max() - st[:, 3].min()) / 100),
            "phase_cycles_median": phases,
            "layer1_wave_marks": waves_l1}  # [entry, contraction done, epilogue done, barrier] cycles
     print(json.dumps(out))

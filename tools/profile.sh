@@ -6,7 +6,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 STEPS=${STEPS:-200}
-ARGS=${ARGS:-"--no-cpu --no-latency"}
+ARGS=${ARGS:-"--no-cpu --no-latency --no-ctl"}
 TAG=${TAG:-mlp}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_kt -o run -- python3 $R/bench.py --steps $STEPS $ARGS > $R/gpurun_out/prof_${TAG}_kt.log 2>&1 || { echo "kt pass failed rc=$?"; exit 1; }
