@@ -1,5 +1,12 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/ -m gpu -q -x > gpurun_out/tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/tests.log; [ $rc = 0 ] || { grep -E "^E |FAILED" gpurun_out/tests.log | head -20; exit 1; }
-timeout -k 10 300 python bench.py > gpurun_out/b.json 2> gpurun_out/b.err || exit 1
-cat gpurun_out/b.json
+TAG=mlp512 STEPS=300 bash tools/profile.sh || exit 1
+TAG=gru256 STEPS=200 ARGS="--no-cpu --no-latency --no-ctl --workload go2_gru_256_b4096" bash tools/profile.sh || exit 1
+TAG=ctl STEPS=50 ARGS="--no-cpu" bash tools/profile.sh || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || exit 1
+export GO2PI_LIB=$PWD/go2_onnx_controller_amd/lib/diag/libgo2pi_clock.so GO2PI_DIAG_STAMPS=1
+timeout -k 10 120 python tools/clock_probe.py > gpurun_out/clock_mlp512.json || exit 1
+timeout -k 10 120 python tools/clock_probe.py --model go2_gru_256 > gpurun_out/clock_gru256.json || exit 1
+timeout -k 10 120 python tools/clock_probe.py --model tests/golden/model.onnx > gpurun_out/clock_shipped.json || exit 1
+timeout -k 10 120 python tools/clock_probe.py --model tests/golden/model.onnx --ctl > gpurun_out/clock_ctl.json || exit 1
+echo done
