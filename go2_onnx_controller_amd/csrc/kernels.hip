@@ -36,6 +36,8 @@ namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
+
 // Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
 //   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
 //   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic
@@ -339,6 +341,11 @@ __device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float
 // X: LDS activations [16][xs], W: this layer's fragments (chunk-major: the
 // float4 stride between consecutive chunks of one tile is TL * 64).
 
+// component j of a float4 (j a compile-time constant after unrolling)
+__device__ __forceinline__ float f4c(const float4 &v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
 // one weight fragment (GO2PI_DIAG_NOLOAD: register arithmetic instead, diagnostics)
 __device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int i) {
 #ifdef GO2PI_DIAG_NOLOAD
@@ -361,34 +368,77 @@ __device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int 
 // order (hipcc otherwise sinks loads next to their uses). Tiles beyond T clamp
 // to T - 1 (duplicate loads, results unused); loads past c1 clamp to c1 - 1.
 // Requires (c1 - c0) % 4 == 0 (K padded to 64).
+//
+// Hand-off between two wide layers without a workgroup barrier (Handoff):
+// wave w publishes flags[w] = ep once its tiles of a layer are stored in LDS;
+// a wave of the next layer starts on the 4-chunk group that its own tiles form
+// (rotated chunk order, g0) and, before reading any group's A operands, waits
+// until that group's producer waves have published ep. A wave therefore reads
+// a group only after its producers stored it (RAW), and every producer sets
+// its flag only after its own contraction of the layer before, which read the
+// buffer this layer's epilogue overwrites (ping-pong WAR): by the end of its
+// contraction a consumer has seen every producer's flag. The rotation changes
+// the summation order of K chunks per wave, identically for every robot row.
+struct Handoff {
+  const int *flags;  // LDS, one int per wave; nullptr: the input is complete (barrier before)
+  int ep;            // epoch every producer of the input must have published
+  int tpw;           // producer tiles per wave
+};
+
+__device__ __forceinline__ void handoff_wait(const Handoff &h, int c, int nw, int lane, bool &all) {
+  if (!h.flags || all) return;
+  const int wlo = c / h.tpw, whi = (c + 3) / h.tpw;  // producers of chunks c..c+3 (= tiles)
+  const unsigned long long need = ((2ull << whi) - 1) & ~((1ull << wlo) - 1);
+  for (int it = 0; it < (1 << 20); ++it) {  // bounded: ~30 ms, a protocol bug must not hang the GPU
+    const int f =
+        lane < nw ? __hip_atomic_load(h.flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : h.ep;
+    const unsigned long long ok = __ballot(f >= h.ep);
+    if (ok == ~0ull) {
+      all = true;  // every producer is done: no further polls this layer
+      break;
+    }
+    if ((ok & need) == need) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // the group's A-operand reads stay after the poll
+}
+
+__device__ __forceinline__ void handoff_publish(int *flags, int wave, int lane, int ep) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
+  if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int TPW>
-__device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, const float4 *__restrict__ W,
-                                          int TL, int t_first, int T, int c0, int c1, int lane,
-                                          f32x4 (&acc)[TPW]) {
+__device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *__restrict__ W, int TL, int t_first,
+                                          int T, int c0, int c1, int lane, f32x4 (&acc)[TPW],
+                                          const Handoff &h = Handoff{nullptr, 0, 1}, int g0 = 0, int nw = 0) {
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const float4 *wp[TPW];
   const int cs = TL * 64;
 #pragma unroll
   for (int i = 0; i < TPW; ++i) wp[i] = W + (size_t)min(t_first + i, T - 1) * 64 + lane;
   if (c0 >= c1) return;
+  const int NG = (c1 - c0) >> 2;
+  int g = g0 % NG;
   float4 cur[TPW];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0, cs, i);
+  for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0 + 4 * g, cs, i);
   // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
   // a trailing load would only be waited for by the epilogue
   // (A operands are read per 4-chunk group; double-buffering them across groups
   // measured slower: 100.4K vs 97.8K cycles per workgroup; fragments 2 chunks
   // ahead instead of 1 measured slower too: 98.1K vs 96.2K)
-  auto group = [&](int c, auto tail_k) {
+  auto group = [&](int c, int cnext, auto tail_k) {
     constexpr bool TAIL = decltype(tail_k)::value;
     float4 a[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int cn = c + u + 1;
+      const int cn = u < 3 ? c + u + 1 : cnext;  // the next group's first chunk (rotated order)
       const bool LOAD = !(TAIL && u == 3);  // folded after unrolling
       float4 nxt[TPW];
+#ifdef GO2PI_DIAG_TILEOUTER  // previous order: each tile's 4 k-steps back to back
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         acc[i] = mfma4(a[u].x, cur[i].x, acc[i]);
@@ -401,15 +451,41 @@ __device__ __forceinline__ void dense_acc(const float *__restrict__ X, int xs, c
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+#else
+      // k-step outer, tile inner: consecutive MFMAs hit different accumulators,
+      // so one wave issues at the 32-cycle rate instead of waiting out the
+      // 40-cycle dependent-accumulator latency. Each accumulator still sees its
+      // k-steps in the same order, so results are bitwise unchanged. One
+      // fragment load after every 4th MFMA: TPW loads spread over 4*TPW MFMAs.
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          acc[i] = mfma4(f4c(a[u], j), f4c(cur[i], j), acc[i]);
+          const int s = j * TPW + i;
+          if (LOAD && (s & 3) == 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            nxt[s >> 2] = load_frag(wp[s >> 2], cn, cs, s >> 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+#endif
       if (LOAD) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
       }
     }
   };
-  int c = c0;
-  for (; c + 4 < c1; c += 4) group(c, std::false_type{});
-  group(c, std::true_type{});
+  bool all = false;
+  for (int k = 0; k + 1 < NG; ++k) {
+    const int gn = g + 1 == NG ? 0 : g + 1;
+    handoff_wait(h, c0 + 4 * g, nw, lane, all);
+    group(c0 + 4 * g, c0 + 4 * gn, std::false_type{});
+    g = gn;
+  }
+  handoff_wait(h, c0 + 4 * g, nw, lane, all);
+  group(c0 + 4 * g, 0, std::true_type{});
 }
 
 // The bias is fetched before the contraction and added in the epilogue, so its
@@ -462,7 +538,7 @@ template <int TPW, int HT>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out,
                                             const CtlView ctl, int row0, int B, const DevLayer *HL,
-                                            f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+                                            f32x4 (&hacc)[HT > 0 ? HT : 1], const Handoff &h, int g0, int nw) {
   constexpr int HN = HT > 0 ? HT : 1;
   f32x4 acc[TPW];
   float bv[TPW];
@@ -484,7 +560,7 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
                                : nullptr;
   if (st) st[0] = __builtin_amdgcn_s_memtime();
 #endif
-  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc);
+  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc, h, g0, nw);
 #ifdef GO2PI_DIAG_CLOCK
   if (st) st[1] = __builtin_amdgcn_s_memtime();
 #endif
@@ -517,7 +593,8 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
                                             int t_first, int T, int C, int lane, bool last, float *out,
                                             const CtlView ctl, int row0, int B) {
   f32x4 none[1];
-  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none);
+  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none,
+                      Handoff{nullptr, 0, 1}, 0, 0);
 }
 
 // Tiles of a wide layer split over the NW waves (full K per wave), optionally
@@ -525,7 +602,8 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 template <int NW, int HT>
 __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int wave, int lane, bool last, float *out, const CtlView ctl, int row0,
-                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
+                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1],
+                                            const Handoff &h) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   // largest tile group per pass: bounded so the accumulators fit the VGPR
   // budget of NW waves per CU (512 / (NW/4) registers per lane)
@@ -537,13 +615,19 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
   const int tpw = (T + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
-  for (; t + G <= t_end; t += G) dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc);
+  const int g0 = h.flags ? (wave * h.tpw) >> 2 : 0;  // the chunk group this wave produced itself
+  for (; t + G <= t_end; t += G)
+    dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
   const int rem = t_end - t;
-  if (G > 4 && rem > 4) dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
+  if (G > 4 && rem > 4)
+    dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
   else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
-  else if (rem == 2) dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
-  else if (rem == 1) dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
+    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0,
+                                     NW);
+  else if (rem == 2)
+    dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
+  else if (rem == 1)
+    dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
 }
 
 // Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
@@ -551,11 +635,11 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
 template <int NW, int HT>
 __device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevLayer &L, const DevLayer &HL,
                                                  const float *X, float *Y, int xs, f32x4 *scratch, int wave,
-                                                 int lane, int row0, int B) {
+                                                 int lane, int row0, int B, const Handoff &hin) {
   f32x4 hacc[HT];
 #pragma unroll
   for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc);
+  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc, hin);
 #pragma unroll
   for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
 }
@@ -577,11 +661,11 @@ __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer 
 template <int NW>
 __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             f32x4 *scratch, int wave, int lane, bool last, float *out,
-                                            const CtlView ctl, int row0, int B) {
+                                            const CtlView ctl, int row0, int B, const Handoff &hin) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
     f32x4 none[1];
-    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none);
+    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none, hin);
   } else {
     // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
     const int ks = NW / T;
@@ -641,6 +725,33 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
   }
   auto step = [&](int c, const float4 &a, f32x4 (&third)[GT], int cn) {
     float4 nz[GT], nr[GT], nh3[GT];
+#ifndef GO2PI_DIAG_TILEOUTER
+    // k-step outer over the 3*GT independent gate accumulators (no back-to-back
+    // dependent MFMA; per-accumulator k order unchanged), one gate-fragment load
+    // after every 4th MFMA
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int i = 0; i < GT; ++i) {
+        z[i] = mfma4(f4c(a, j), f4c(cz[i], j), z[i]);
+        r[i] = mfma4(f4c(a, j), f4c(cr[i], j), r[i]);
+        third[i] = mfma4(f4c(a, j), f4c(chh[i], j), third[i]);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const int s = (j * GT + i) * 3 + g;
+          if ((s & 3) == 3) {
+            const int q = s >> 2, ti = q / 3, gi = q % 3;
+            __builtin_amdgcn_sched_barrier(0);
+            const float4 f = wp[ti][cn * cs + 64 * gi];
+            if (gi == 0) nz[ti] = f;
+            else if (gi == 1) nr[ti] = f;
+            else nh3[ti] = f;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+#else
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
       z[i] = mfma4(a.x, cz[i].x, z[i]);
@@ -665,6 +776,7 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
       nh3[i] = wp[i][cn * cs + 128];
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
       cz[i] = nz[i];
@@ -741,8 +853,13 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 
   // controller tick: this tile's raw inputs staged in LDS behind the scratch
   // region (one burst of direct-to-LDS loads), then assembled from there
-  const CtlLds CL = ctl_lds(lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S + 256 * NW * (P.head_fuse > 1 ? P.head_fuse : 1),
-                            GO2PI_TILE_ROWS, P.in_dim);
+  // per-wave layer hand-off flags (Handoff) behind the scratch region, cleared
+  // here; every path passes a workgroup barrier before the first layer
+  float *after_scratch = lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S + 256 * NW * (P.head_fuse > 1 ? P.head_fuse : 1);
+  int *flags = reinterpret_cast<int *>(after_scratch);
+  if (tid < NW) flags[tid] = 0;
+  int ep = 0;  // hand-offs published so far (identical in every wave)
+  const CtlLds CL = ctl_lds(after_scratch + GO2PI_FLAG_FLOATS, GO2PI_TILE_ROWS, P.in_dim);
   CtlView cv{};
   CtlQ cq{};
   if constexpr (CTL) {
@@ -830,11 +947,13 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       // no barrier needed: layer 0 below reads bufB (X) and writes bufA (Y); bufH is
       // next read after the end-of-step barrier
     }
+    Handoff hin{nullptr, 0, 1};  // layer input complete: the barrier above
     for (int l = 0; l < P.nl; ++l) {
       const bool last = l == P.nl - 1;
       if (P.head_fuse && l == P.nl - 2) {
-        if (P.head_fuse == 1) dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
-        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
+        if (P.head_fuse == 1)
+          dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
+        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
         __syncthreads();
         head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, cv, row0, B);
 #ifdef GO2PI_DIAG_CLOCK
@@ -845,8 +964,26 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 #endif
         break;  // scratch is next written two barriers later; bufA/bufB are free
       }
-      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B);
-      __syncthreads();
+      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B, hin);
+      // two wide layers in a row (both split by tiles over the waves, no split-K)
+      // hand off through per-wave flags instead of a workgroup barrier
+      const int T = P.L[l].N_pad >> 4;
+#ifdef GO2PI_DIAG_HANDOFF
+      // variant (diagnostics): flag hand-off between two wide layers. Measured
+      // slower than the barrier on MI355X (mlp512: 47.8 vs 45.6 us per launch;
+      // gru256: 78.4 vs 76.4 us), so the shipped build keeps the barrier.
+      const bool flag_next = !last && T >= NW && (P.L[l + 1].N_pad >> 4) >= NW;
+#else
+      const bool flag_next = false;  // a workgroup barrier after every layer
+#endif
+      if (flag_next) {
+        ++ep;
+        handoff_publish(flags, wave, lane, ep);
+        hin = Handoff{flags, ep, (T + NW - 1) / NW};
+      } else {
+        __syncthreads();
+        hin = Handoff{nullptr, 0, 1};
+      }
 #ifdef GO2PI_DIAG_CLOCK
       if (tid == 0 && P.stamps && step == 0 && l < 10)
         P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
@@ -1192,8 +1329,9 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 // ---------------------------------------------------------------------------
 size_t fused_lds_bytes(const DevProgram &p, int waves) {
   // activation buffers + per-wave partial-sum scratch (head fusion: up to 2 tiles)
+  // + the layer hand-off flags
   return sizeof(float) * (size_t)(2 + p.has_gru) * GO2PI_TILE_ROWS * p.lds_stride +
-         sizeof(f32x4) * 64 * waves * (p.head_fuse > 1 ? p.head_fuse : 1);
+         sizeof(f32x4) * 64 * waves * (p.head_fuse > 1 ? p.head_fuse : 1) + sizeof(float) * GO2PI_FLAG_FLOATS;
 }
 
 size_t gemv_lds_bytes(const DevProgram &p, int layer) {
