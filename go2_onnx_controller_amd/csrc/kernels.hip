@@ -383,7 +383,27 @@ struct Handoff {
   const int *flags;  // LDS, one int per wave; nullptr: the input is complete (barrier before)
   int ep;            // epoch every producer of the input must have published
   int tpw;           // producer tiles per wave
+  // cross-layer prefetch (barrier hand-off only): this wave's first tile
+  // group's chunk-0 fragments, loaded before the barrier (prefetch_first)
+  float4 pre[4];
+  int npre;  // valid entries of pre (0: none)
 };
+
+// Issue this wave's first weight fragments of layer L (chunk 0 of its first
+// tile group) before the barrier that completes L's input: they do not depend
+// on the activations, and the barrier waits on LDS only (lgkmcnt), so the
+// loads stay in flight across it. Same addresses as dense_acc's first loads.
+template <int NW>
+__device__ __forceinline__ void prefetch_first(const DevLayer &L, int wave, int lane, Handoff &h) {
+  const int T = L.N_pad >> 4;
+  if (T < NW) return;  // narrow layer: split-K path, no tile groups
+  constexpr int NP = NW >= 16 ? 2 : 4;  // min(G, 4)
+  const int t = wave * ((T + NW - 1) / NW);
+  const float4 *W = reinterpret_cast<const float4 *>(L.w);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) h.pre[i] = load_frag(W + (size_t)min(t + i, T - 1) * 64 + lane, 0, 0, i);
+  h.npre = NP;
+}
 
 __device__ __forceinline__ void handoff_wait(const Handoff &h, int c, int nw, int lane, bool &all) {
   if (!h.flags || all) return;
@@ -421,8 +441,13 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
   const int NG = (c1 - c0) >> 2;
   int g = g0 % NG;
   float4 cur[TPW];
+  if (TPW <= 4 && !h.flags && h.npre >= TPW && c0 == 0) {
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0 + 4 * g, cs, i);
+    for (int i = 0; i < TPW; ++i) cur[i] = h.pre[i < 4 ? i : 0];  // prefetched before the barrier
+  } else {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0 + 4 * g, cs, i);
+  }
   // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
   // a trailing load would only be waited for by the epilogue
   // (A operands are read per 4-chunk group; double-buffering them across groups
@@ -616,18 +641,21 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
   const int g0 = h.flags ? (wave * h.tpw) >> 2 : 0;  // the chunk group this wave produced itself
-  for (; t + G <= t_end; t += G)
-    dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
+  Handoff hh = h;  // prefetched fragments (hh.npre) belong to the first group only
+  for (; t + G <= t_end; t += G) {
+    dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    hh.npre = 0;
+  }
   const int rem = t_end - t;
   if (G > 4 && rem > 4)
-    dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
+    dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
   else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0,
+    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0,
                                      NW);
   else if (rem == 2)
-    dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
+    dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
   else if (rem == 1)
-    dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, h, g0, NW);
+    dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
 }
 
 // Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
@@ -981,8 +1009,11 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         handoff_publish(flags, wave, lane, ep);
         hin = Handoff{flags, ep, (T + NW - 1) / NW};
       } else {
-        __syncthreads();
         hin = Handoff{nullptr, 0, 1};
+#ifdef GO2PI_DIAG_PREFETCH  // variant (diagnostics): measured slower, see DESIGN §4.1
+        if (!last) prefetch_first<NW>(P.L[l + 1], wave, lane, hin);
+#endif
+        __syncthreads();
       }
 #ifdef GO2PI_DIAG_CLOCK
       if (tid == 0 && P.stamps && step == 0 && l < 10)
