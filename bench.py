@@ -183,16 +183,18 @@ def controller_leg(device, steps=200, warm=20, iters=3000):
     return out
 
 
-def load_pmc(workload, kernel_substr, waves):
-    """Memory-side bytes per launch of `kernel_substr` from the committed rocprofv3
-    --pmc summary of this workload (tools/profile.sh + tools/summarize_prof.py:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction x2)."""
+def load_pmc(workload, kernel):
+    """Memory-side bytes per launch of the batched kernel instantiation `kernel`
+    (e.g. "policy_fused_kernel<4, 8, 1>", Engine.batched_kernel) from the
+    committed rocprofv3 --pmc summary of this workload (tools/profile.sh +
+    tools/summarize_prof.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read
+    correction x2). None when no summary of this exact kernel is committed."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
         for k, v in d.get("workloads", {}).get(workload, {}).items():
-            if kernel_substr in k and f"<{waves}>" in k:
+            if f"::{kernel}(" in k:
                 return v.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -283,7 +285,8 @@ def main():
     flops_launch = cost["flops_per_row"] * batch
     bytes_launch = cost["weight_bytes"] + cost["io_bytes_per_row"] * batch
     achieved_tf = flops_launch / (kernel_ms * 1e-3) / 1e12
-    traffic = load_pmc(args.workload, "policy_fused_kernel", args.waves or 8)
+    kernel_name = eng.batched_kernel
+    traffic = load_pmc(args.workload, kernel_name)
     eng.close()
 
     out = {
@@ -302,6 +305,7 @@ def main():
                 if mname != "__shipped__" else "synthetic obs N(0,1); shipped reference weights",
         "config": {"workload": args.workload, "description": cfg_desc, "robots_per_gpu": batch,
                    "global_batch": batch * world, "parallelism": f"fleet shards x{world} (no data-path collective)"},
+        "kernel": kernel_name,
         "kernel_us": round(kernel_ms * 1e3, 3),
         "host_enqueue_us": round(host_us, 3),
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,

@@ -369,6 +369,22 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     const int t_last = p.L[p.nl - 1].N_pad / 16, t_prev = p.L[p.nl - 2].N_pad / 16;
     if (t_last <= 2 && t_prev >= e.waves) p.head_fuse = t_last;
   }
+  // 4-wave uniform-MLP pipeline (kernels.hip, w4_step): no GRU, a fused head, and
+  // every hidden layer exactly one group of 2, 4 or 8 tiles per wave. It is the
+  // default (waves = 0) wherever it applies: measured faster than the generic
+  // 8-wave body; otherwise waves = 0 means 8.
+  if ((e.opts.waves == 0 || e.opts.waves == 4) && p.nl >= 2 && !m.has_gru && !std::getenv("GO2PI_NO_HEAD_FUSE") &&
+      !std::getenv("GO2PI_NO_W4")) {  // env: A/B diagnostics only
+    const int t_last = p.L[p.nl - 1].N_pad / 16;
+    const int tpw = p.L[0].N_pad / 64;
+    bool uniform = (tpw == 2 || tpw == 4 || tpw == 8) && t_last <= (tpw == 8 ? 1 : 2);
+    for (int l = 0; l + 1 < p.nl; ++l) uniform = uniform && p.L[l].N_pad == 64 * tpw;
+    if (uniform) {
+      e.waves = 4;
+      p.head_fuse = t_last;
+      p.w4_tpw = tpw;
+    }
+  }
 
   // prologue: model-defined (Sub/Div nodes) and/or opts-defined normalisation
   std::vector<float> sub = m.pre_sub, div = m.pre_div;
@@ -887,6 +903,16 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *c) {
     check_engine(e);
     if (!c) throw ApiError("null cost", GO2PI_E_INVALID);
     *c = e->cost;
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
+  return guarded([&] {
+    check_engine(e);
+    if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
+    const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
+    std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d>", e->waves, t, h);
     return GO2PI_OK;
   });
 }

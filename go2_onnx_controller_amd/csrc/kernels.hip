@@ -36,6 +36,22 @@ namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#if defined(GO2PI_DIAG_RD1)
+#define GO2PI_RING_RD 1
+#elif defined(GO2PI_DIAG_RD3)
+#define GO2PI_RING_RD 3
+#else
+#define GO2PI_RING_RD 2  // chunks ahead of the weight-fragment ring at 4 waves per workgroup
+#endif
+#ifndef GO2PI_WPOL  // weight-fragment load policy: 0 plain, 1 nt, 2 sc1 (L1 bypass)
+#if defined(GO2PI_DIAG_NT)
+#define GO2PI_WPOL 1
+#elif defined(GO2PI_DIAG_SC1)
+#define GO2PI_WPOL 2
+#else
+#define GO2PI_WPOL 0
+#endif
+#endif
 #define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
 
 // Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
@@ -353,10 +369,32 @@ __device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int 
   (void)p;
   (void)cs;
   return make_float4(v, v, v, v);
+#elif GO2PI_WPOL == 1
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p + c * cs));
+  return make_float4(v.x, v.y, v.z, v.w);
 #else
   return p[c * cs];
 #endif
 }
+
+// Weight-fragment stream over a buffer resource: one SGPR descriptor per layer,
+// a per-lane byte offset per tile and the chunk offset folded into the scalar
+// offset. GO2PI_WPOL == 2 sets sc1 on the loads (served by the XCD's L2,
+// bypassing the CU's 32 KiB L1, which the fragments in flight would overrun).
+struct WStream {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit WStream(const void *base)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000)) {}
+  __device__ __forceinline__ float4 ld(int voff, int soff) const {
+#ifdef GO2PI_DIAG_NOLOAD
+    const float v = __int_as_float(0x3c000000 ^ ((voff + soff) & 0xff));
+    return make_float4(v, v, v, v);
+#else
+    constexpr int AUX = GO2PI_WPOL == 2 ? 16 : (GO2PI_WPOL == 1 ? 2 : 0);
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+#endif
+  }
+};
 
 // Schedule (measured on MI355X with tools/clock_probe.py, cycles per 16-robot
 // workgroup of the 48->512^3->12 step): every tile's fragment for chunk c+1 is
@@ -433,10 +471,11 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
                                           int T, int c0, int c1, int lane, f32x4 (&acc)[TPW],
                                           const Handoff &h = Handoff{nullptr, 0, 1}, int g0 = 0, int nw = 0) {
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  const float4 *wp[TPW];
-  const int cs = TL * 64;
+  const WStream ws(W);
+  int vo[TPW];                // per-lane byte offset of each tile's fragment in chunk 0
+  const int csb = TL * 1024;  // bytes per chunk (all tiles)
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) wp[i] = W + (size_t)min(t_first + i, T - 1) * 64 + lane;
+  for (int i = 0; i < TPW; ++i) vo[i] = (min(t_first + i, T - 1) * 64 + lane) * 16;
   if (c0 >= c1) return;
   const int NG = (c1 - c0) >> 2;
   int g = g0 % NG;
@@ -446,7 +485,7 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
     for (int i = 0; i < TPW; ++i) cur[i] = h.pre[i < 4 ? i : 0];  // prefetched before the barrier
   } else {
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) cur[i] = load_frag(wp[i], c0 + 4 * g, cs, i);
+    for (int i = 0; i < TPW; ++i) cur[i] = ws.ld(vo[i], (c0 + 4 * g) * csb);
   }
   // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
   // a trailing load would only be waited for by the epilogue
@@ -466,13 +505,13 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
 #ifdef GO2PI_DIAG_TILEOUTER  // previous order: each tile's 4 k-steps back to back
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
-        acc[i] = mfma4(a[u].x, cur[i].x, acc[i]);
-        acc[i] = mfma4(a[u].y, cur[i].y, acc[i]);
-        acc[i] = mfma4(a[u].z, cur[i].z, acc[i]);
-        acc[i] = mfma4(a[u].w, cur[i].w, acc[i]);
+        acc[i] = mfma4(cur[i].x, a[u].x, acc[i]);
+        acc[i] = mfma4(cur[i].y, a[u].y, acc[i]);
+        acc[i] = mfma4(cur[i].z, a[u].z, acc[i]);
+        acc[i] = mfma4(cur[i].w, a[u].w, acc[i]);
         if (LOAD) {
           __builtin_amdgcn_sched_barrier(0);
-          nxt[i] = load_frag(wp[i], cn, cs, i);
+          nxt[i] = ws.ld(vo[i], cn * csb);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -486,11 +525,11 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
       for (int j = 0; j < 4; ++j) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-          acc[i] = mfma4(f4c(a[u], j), f4c(cur[i], j), acc[i]);
+          acc[i] = mfma4(f4c(cur[i], j), f4c(a[u], j), acc[i]);
           const int s = j * TPW + i;
           if (LOAD && (s & 3) == 3) {
             __builtin_amdgcn_sched_barrier(0);
-            nxt[s >> 2] = load_frag(wp[s >> 2], cn, cs, s >> 2);
+            nxt[s >> 2] = ws.ld(vo[s >> 2], cn * csb);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -513,22 +552,90 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
   group(c0 + 4 * g, 0, std::true_type{});
 }
 
+// Contraction for one wave per SIMD (4 waves per workgroup): a wave owns TPW
+// tiles over the full K and nothing on its SIMD competes for the matrix pipe,
+// so the schedule must hide every latency by itself:
+//   * weight fragments stream RD chunks ahead through a 4-slot register ring
+//     (slot = chunk % 4): the fragment an MFMA consumes was issued >= RD - 1
+//     chunks (>= (RD - 1) * 4 * TPW MFMAs) earlier;
+//   * the A operand of chunk c + 1 is read from LDS during chunk c;
+//   * loads are spread one per 4 MFMAs (sched_barrier pins them in place).
+// The k-step / tile order is the same as dense_acc's, so every accumulator sees
+// its k-steps in the same order: results are bitwise those of dense_acc.
+// Requires C % 4 == 0 (K padded to 64) and C >= 4.
+template <int TPW, int RD>
+__device__ __forceinline__ void dense_acc_ring(const float *X, int xs, const float4 *__restrict__ W, int TL,
+                                               int t_first, int T, int C, int lane, f32x4 (&acc)[TPW]) {
+  static_assert(RD >= 1 && RD <= 3, "ring of 4 slots: at most 3 chunks ahead");
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const WStream ws(W);
+  int vo[TPW];                // per-lane byte offset of each tile's fragment in chunk 0
+  const int csb = TL * 1024;  // bytes per chunk (all tiles)
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) vo[i] = (min(t_first + i, T - 1) * 64 + lane) * 16;
+  float4 f[4][TPW];
+  float4 a[2];
+#pragma unroll
+  for (int d = 0; d < RD; ++d)
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) f[d][i] = ws.ld(vo[i], d * csb);
+  a[0] = *reinterpret_cast<const float4 *>(xrow);
+  // one 4-chunk group; TAIL: the last one (no loads past C)
+  auto group = [&](int c0, auto tail_k) {
+    constexpr bool TAIL = decltype(tail_k)::value;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u;
+      if (!(TAIL && u == 3)) a[(u + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
+      const bool LOAD = !(TAIL && u + RD >= 4);  // chunk c + RD exists (folded after unrolling)
+      constexpr int NS = 4 * TPW;                 // MFMAs per chunk
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          acc[i] = mfma4(f4c(f[u][i], j), f4c(a[u & 1], j), acc[i]);
+          const int s = j * TPW + i;
+          if (LOAD && (s % (NS / TPW)) == (NS / TPW) - 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            f[(u + RD) & 3][s / (NS / TPW)] = ws.ld(vo[s / (NS / TPW)], (c + RD) * csb);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  };
+  int c0 = 0;
+  for (; c0 + 4 < C; c0 += 4) group(c0, std::false_type{});
+  group(c0, std::true_type{});
+}
+
+// Accumulator layout of the dense path ("output-major"): the weight fragment is
+// the MFMA's A operand and the activations its B operand, so D = W_tile . X^T
+// and lane l holds outputs n = 16t + 4(l >> 4) + r (r = 0..3) of robot l & 15:
+// four consecutive outputs of one robot, i.e. one float4 of its activation row.
+// (The product and the per-accumulator k order are those of X . W^T: results
+// are bitwise the same as with the operands the other way round.)
+
 // The bias is fetched before the contraction and added in the epilogue, so its
 // load latency hides behind the MFMA loop instead of delaying the first MFMA.
 template <int TPW>
-__device__ __forceinline__ void load_bias(float (&bv)[TPW], const float *__restrict__ bias, int t_first, int T,
+__device__ __forceinline__ void load_bias(float4 (&bv)[TPW], const float *__restrict__ bias, int t_first, int T,
                                           int lane) {
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) bv[i] = bias[min(t_first + i, T - 1) * 16 + (lane & 15)];
+  for (int i = 0; i < TPW; ++i)
+    bv[i] = *reinterpret_cast<const float4 *>(bias + min(t_first + i, T - 1) * 16 + ((lane >> 4) << 2));
 }
 
-// Epilogue of a hidden layer: bias + activation, write the 16 x 16 tile to LDS.
-// Epilogue of the final layer: bias + activation + post, write valid rows/cols to HBM.
-template <int TPW>
+// Epilogue of a hidden layer: bias + activation, one float4 per tile and lane to
+// the LDS activation row (one ds_write_b128 instead of four ds_write_b32); the
+// activated values also go to `keep` (head fusion consumes them from registers).
+// Epilogue of the final layer: bias + activation + post, valid rows/cols to HBM.
+template <int TPW, bool KEEP = false>
 __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW],
-                                            const float (&bv)[TPW], int t_first, int T, int lane, bool last, float *Y,
-                                            int ys, float *out, const CtlView ctl, int row0, int B) {
-  const int col = lane & 15, r0 = (lane >> 4) << 2;
+                                            const float4 (&bv)[TPW], int t_first, int T, int lane, bool last,
+                                            float *Y, int ys, float *out, const CtlView ctl, int row0, int B,
+                                            float4 (&keep)[TPW]) {
+  const int rob = lane & 15, n0 = (lane >> 4) << 2;
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
     const float alpha = L.alpha;
@@ -536,18 +643,24 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
     for (int i = 0; i < TPW; ++i) {
       const int t = t_first + i;
       if (t >= T) continue;
-      const int n = t * 16 + col;
+      float4 v;
+      v.x = act_t<ACT>(alpha, acc[i][0] + bv[i].x);
+      v.y = act_t<ACT>(alpha, acc[i][1] + bv[i].y);
+      v.z = act_t<ACT>(alpha, acc[i][2] + bv[i].z);
+      v.w = act_t<ACT>(alpha, acc[i][3] + bv[i].w);
       if (!last) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Y[(r0 + r) * ys + n] = act_t<ACT>(alpha, acc[i][r] + bv[i]);
-      } else if (n < L.N) {
+        *reinterpret_cast<float4 *>(Y + rob * ys + t * 16 + n0) = v;
+        if constexpr (KEEP) keep[i] = v;
+      } else {
+        const int row = row0 + rob;
+        if (row >= B) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = row0 + r0 + r;
-          if (row >= B) continue;
-          const float v = post_fn(P, act_t<ACT>(alpha, acc[i][r] + bv[i]));
-          if (ctl.on) ctl_store(ctl, row, n, v);  // controller tick: action post-processing
-          else out[(size_t)row * L.N + n] = v;
+          const int n = t * 16 + n0 + r;
+          if (n >= L.N) continue;
+          const float y = post_fn(P, f4c(v, r));
+          if (ctl.on) ctl_store(ctl, row, n, y);  // controller tick: action post-processing
+          else out[(size_t)row * L.N + n] = y;
         }
       }
     }
@@ -559,14 +672,14 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
 // tiles are exactly its K-chunks of HL, so it multiplies them (read back from
 // LDS by the same wave) against HL's fragments, fetched before its MFMA loop.
 // Partials are summed across waves in a fixed order by head_finish (below).
-template <int TPW, int HT>
+template <int TPW, int HT, int RD = 0>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out,
                                             const CtlView ctl, int row0, int B, const DevLayer *HL,
                                             f32x4 (&hacc)[HT > 0 ? HT : 1], const Handoff &h, int g0, int nw) {
   constexpr int HN = HT > 0 ? HT : 1;
   f32x4 acc[TPW];
-  float bv[TPW];
+  float4 bv[TPW];
   float4 hw[HN][TPW];
   load_bias<TPW>(bv, L.bias, t_first, T, lane);
   if constexpr (HT > 0) {
@@ -585,29 +698,31 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
                                : nullptr;
   if (st) st[0] = __builtin_amdgcn_s_memtime();
 #endif
-  dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc, h, g0, nw);
+  if constexpr (RD > 0)
+    dense_acc_ring<TPW, RD>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, C, lane, acc);
+  else
+    dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc, h, g0,
+                   nw);
 #ifdef GO2PI_DIAG_CLOCK
   if (st) st[1] = __builtin_amdgcn_s_memtime();
 #endif
-  dense_store<TPW>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, ctl, row0, B);
+  float4 yv[TPW];
+  dense_store<TPW, (HT > 0)>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, ctl, row0, B, yv);
 #ifdef GO2PI_DIAG_CLOCK
   if (st) st[2] = __builtin_amdgcn_s_memtime();
 #endif
   if constexpr (HT > 0) {
-    // this wave's own LDS stores above are read back below (other lanes' values):
-    // keep the compiler from hoisting the reads (the LDS queue is in order per wave)
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const float *yrow = Y + (lane & 15) * xs + ((lane >> 4) << 2);
+    // the head's B operand for k-chunk t_first + i is exactly the float4 this
+    // lane just stored (its robot, k = 16t + 4(lane >> 4) + j): use the registers
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       if (t_first + i >= T) continue;
-      const float4 a = *reinterpret_cast<const float4 *>(yrow + (t_first + i) * 16);
 #pragma unroll
       for (int h = 0; h < HT; ++h) {
-        hacc[h] = mfma4(a.x, hw[h][i].x, hacc[h]);
-        hacc[h] = mfma4(a.y, hw[h][i].y, hacc[h]);
-        hacc[h] = mfma4(a.z, hw[h][i].z, hacc[h]);
-        hacc[h] = mfma4(a.w, hw[h][i].w, hacc[h]);
+        hacc[h] = mfma4(hw[h][i].x, yv[i].x, hacc[h]);
+        hacc[h] = mfma4(hw[h][i].y, yv[i].y, hacc[h]);
+        hacc[h] = mfma4(hw[h][i].z, yv[i].z, hacc[h]);
+        hacc[h] = mfma4(hw[h][i].w, yv[i].w, hacc[h]);
       }
     }
   }
@@ -637,25 +752,27 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
 #else
   constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
 #endif
+  // one wave per SIMD: the register-ring contraction (dense_acc_ring)
+  constexpr int RD = NW == 4 ? GO2PI_RING_RD : 0;
   const int tpw = (T + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
   const int g0 = h.flags ? (wave * h.tpw) >> 2 : 0;  // the chunk group this wave produced itself
   Handoff hh = h;  // prefetched fragments (hh.npre) belong to the first group only
   for (; t + G <= t_end; t += G) {
-    dense_group<G, HT>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<G, HT, RD>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
     hh.npre = 0;
   }
   const int rem = t_end - t;
   if (G > 4 && rem > 4)
-    dense_group<G, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<G, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
   else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0,
+    dense_group<(G > 4 ? 4 : G), HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0,
                                      NW);
   else if (rem == 2)
-    dense_group<2, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<2, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
   else if (rem == 1)
-    dense_group<1, HT>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<1, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
 }
 
 // Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
@@ -679,9 +796,10 @@ __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer 
   if (wave >= T) return;
   f32x4 acc[1] = {scratch[(wave * NW) * 64 + lane]};
   for (int w = 1; w < NW; ++w) acc[0] += scratch[(wave * NW + w) * 64 + lane];  // fixed order: deterministic
-  float bv[1];
+  float4 bv[1];
   load_bias<1>(bv, HL.bias, wave, T, lane);
-  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, ctl, row0, B);
+  float4 none[1];
+  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, ctl, row0, B, none);
 }
 
 // One dense layer for the whole workgroup (NW waves). Contains barriers only in
@@ -699,7 +817,7 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
     const int ks = NW / T;
     const int t = wave % T, s = wave / T;
     f32x4 acc[1];
-    float bv[1];
+    float4 bv[1];
     load_bias<1>(bv, L.bias, t, T, lane);
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (s < ks) {
@@ -711,7 +829,8 @@ __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer 
     __syncthreads();
     if (s == 0) {
       for (int s2 = 1; s2 < ks; ++s2) acc[0] += scratch[(t + s2 * T) * 64 + lane];
-      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, ctl, row0, B);
+      float4 none[1];
+      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, ctl, row0, B, none);
     }
   }
 }
@@ -845,10 +964,196 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
   for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Uniform-MLP pipeline at one wave per SIMD (4 waves per workgroup, engine
+// option waves = 4): every hidden layer is exactly one tile group per wave
+// (N_pad = 64 * TPW) and the final layer is fused as the head (HT tiles). The
+// weight-fragment register ring of dense_acc_ring runs ACROSS layer
+// boundaries: the tail of layer l's contraction issues layer l + 1's first RD
+// chunks, and layer 0's are issued before the barrier that completes the
+// observation tile, so no layer starts on an L2 round trip. Per-accumulator k
+// order, epilogue and head are those of the generic path (bitwise the same
+// results as dense_group at 4 waves).
+
+template <int TPW, int RD>
+__device__ __forceinline__ void w4_prefetch(const DevLayer &L, int t0, int lane, float4 (&f)[4][TPW]) {
+  const WStream ws(L.w);
+  const int csb = (L.N_pad >> 4) * 1024;
+#pragma unroll
+  for (int d = 0; d < RD; ++d)
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) f[d][i] = ws.ld(((t0 + i) * 64 + lane) * 16, d * csb);
+}
+
+// Contraction of layer L for tiles [t0, t0 + TPW) over all C = K_pad / 16 chunks.
+// On entry f holds chunks 0 .. RD - 1 in slots 0 .. RD - 1 (chunk c lives in slot
+// c & 3; C % 4 == 0). NEXT: the tail issues NL's chunks 0 .. RD - 1 into the
+// slots the loop has freed, which are slots 0 .. RD - 1 again.
+template <int TPW, int RD, bool NEXT>
+__device__ __forceinline__ void w4_contract(const float *X, int xs, const DevLayer &L, const DevLayer &NL, int t0,
+                                            int lane, f32x4 (&acc)[TPW], float4 (&f)[4][TPW]) {
+  const int C = L.K_pad >> 4;
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const WStream ws(L.w), wn(NL.w);
+  const int csb = (L.N_pad >> 4) * 1024, csn = (NL.N_pad >> 4) * 1024;
+  int vo[TPW];  // same tiles of L and NL: per-lane byte offset in chunk 0
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
+  float4 a[2];
+  a[0] = *reinterpret_cast<const float4 *>(xrow);
+  auto group = [&](int c0, auto tail_k) {
+    constexpr bool TAIL = decltype(tail_k)::value;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u;
+      if (!(TAIL && u == 3)) a[(u + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
+      const bool OWN = !(TAIL && u + RD >= 4);  // chunk c + RD of this layer exists
+      const bool LOAD = OWN || NEXT;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          acc[i] = mfma4(f4c(f[u][i], j), f4c(a[u & 1], j), acc[i]);
+          const int s = j * TPW + i;
+          if (LOAD && (s & 3) == 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (OWN) f[(u + RD) & 3][s >> 2] = ws.ld(vo[s >> 2], (c + RD) * csb);
+            else f[(u + RD) & 3][s >> 2] = wn.ld(vo[s >> 2], (u + RD - 4) * csn);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  };
+  int c0 = 0;
+  for (; c0 + 4 < C; c0 += 4) group(c0, std::false_type{});
+  group(c0, std::true_type{});
+}
+
+// Epilogue of a pipeline hidden layer: every tile is valid (no bounds checks),
+// all TPW activated float4s are computed before the first LDS store, and alpha
+// comes in a register, so the stores go out back to back with no scalar-load
+// wait between them (lgkmcnt counts LDS and scalar loads together).
+template <int TPW, bool KEEP>
+__device__ __forceinline__ void w4_store(int act, float alpha, const f32x4 (&acc)[TPW], const float4 (&bv)[TPW],
+                                         float *Y, int ys, int t0, int lane, float4 (&keep)[TPW]) {
+  float *yrow = Y + (lane & 15) * ys + t0 * 16 + ((lane >> 4) << 2);
+  with_act(act, [&](auto act_k) {
+    constexpr int ACT = decltype(act_k)::value;
+    float4 v[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      v[i].x = act_t<ACT>(alpha, acc[i][0] + bv[i].x);
+      v[i].y = act_t<ACT>(alpha, acc[i][1] + bv[i].y);
+      v[i].z = act_t<ACT>(alpha, acc[i][2] + bv[i].z);
+      v[i].w = act_t<ACT>(alpha, acc[i][3] + bv[i].w);
+    }
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) keep[i] = v[i];
+    }
+  });
+}
+
+// One policy step of the pipeline (the observation tile is being staged into X).
+template <int TPW, int HT, bool CTL>
+__device__ __forceinline__ void w4_step(const DevProgram &P, float *X, float *Y, int S, f32x4 *scratch, int wave,
+                                        int lane, float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
+                                        const CtlLds &CL, int step) {
+  constexpr int RD = GO2PI_RING_RD;
+  const int t0 = wave * TPW;
+  float4 f[4][TPW];
+  w4_prefetch<TPW, RD>(P.L[0], t0, lane, f);
+  __syncthreads();  // the observation tile is complete in X
+#ifdef GO2PI_DIAG_CLOCK
+  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
+#endif
+  if constexpr (CTL) {
+    if (ctl.status && (int)threadIdx.x < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + threadIdx.x] = CL.nanf[threadIdx.x];
+#ifdef GO2PI_DIAG_CLOCK
+    if (threadIdx.x == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
+#endif
+  }
+  const int nh = P.nl - 1;  // hidden layers; P.L[nh] is the fused head
+  for (int l = 0; l < nh; ++l) {
+    const DevLayer &L = P.L[l];
+    const int T = L.N_pad >> 4;
+    const int act = L.act;
+    const float alpha = L.alpha;
+    float4 bv[TPW];
+    load_bias<TPW>(bv, L.bias, t0, T, lane);
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef GO2PI_DIAG_CLOCK
+    unsigned long long *st = (P.stamps && l == 1 && lane == 0)
+                                 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave
+                                 : nullptr;
+    if (st) st[0] = __builtin_amdgcn_s_memtime();
+#endif
+    if (l + 1 < nh) {
+      w4_contract<TPW, RD, true>(X, S, L, P.L[l + 1], t0, lane, acc, f);
+#ifdef GO2PI_DIAG_CLOCK
+      if (st) st[1] = __builtin_amdgcn_s_memtime();
+#endif
+      float4 none[TPW];
+      w4_store<TPW, false>(act, alpha, acc, bv, Y, S, t0, lane, none);
+#ifdef GO2PI_DIAG_CLOCK
+      if (st) st[2] = __builtin_amdgcn_s_memtime();
+#endif
+    } else {
+      const DevLayer &HL = P.L[nh];
+      const float4 *HW = reinterpret_cast<const float4 *>(HL.w);
+      const int HTL = HL.N_pad >> 4;
+      float4 hw[HT][TPW];
+#pragma unroll
+      for (int h = 0; h < HT; ++h)
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)(t0 + i) * HTL + h) * 64 + lane];
+      w4_contract<TPW, RD, false>(X, S, L, L, t0, lane, acc, f);
+#ifdef GO2PI_DIAG_CLOCK
+      if (st) st[1] = __builtin_amdgcn_s_memtime();
+#endif
+      float4 yv[TPW];
+      w4_store<TPW, true>(act, alpha, acc, bv, Y, S, t0, lane, yv);
+#ifdef GO2PI_DIAG_CLOCK
+      if (st) st[2] = __builtin_amdgcn_s_memtime();
+#endif
+      f32x4 hacc[HT];
+#pragma unroll
+      for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+#pragma unroll
+        for (int h = 0; h < HT; ++h) {
+          hacc[h] = mfma4(hw[h][i].x, yv[i].x, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].y, yv[i].y, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].z, yv[i].z, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].w, yv[i].w, hacc[h]);
+        }
+#pragma unroll
+      for (int h = 0; h < HT; ++h) scratch[(h * 4 + wave) * 64 + lane] = hacc[h];
+    }
+    __syncthreads();
+#ifdef GO2PI_DIAG_CLOCK
+    if (threadIdx.x == 0 && P.stamps && step == 0 && l < 8) {
+      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
+      if (l + 1 == nh) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    float *t = X;
+    X = Y;
+    Y = t;
+  }
+  head_finish<4>(P, P.L[nh], scratch, wave, lane, ac, cv, row0, B);
+}
+
 // Body of the batched kernel. CTL: controller tick (steps == 1) — the
 // observation is assembled from raw robot state (ctl_assemble) instead of
 // read, and the final layer's store is the action post-processing (ctl_store).
-template <int NW, bool CTL>
+template <int NW, bool CTL, int W4T = 0, int W4H = 0>
 __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
                                            float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
                                            const DevCtl ctl) {
@@ -864,6 +1169,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
   const int H = P.gru.H;
+#ifdef GO2PI_DIAG_PRIO  // variant: static priority for the second-dispatched half of the waves
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // Touch every layer descriptor up front: one burst of scalar loads warms the
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
@@ -952,6 +1260,11 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   for (int step = 0; step < steps; ++step) {
     float *ac = act + (size_t)step * B * P.out_dim;
     if (step > 0) stage_obs(step);
+    if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
+      static_assert(NW == 4, "one wave per SIMD");
+      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, wave, lane, ac, cv, row0, B, ctl, CL, step);
+      continue;
+    }
     __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
     if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
@@ -1038,17 +1351,20 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 #endif
 }
 
-template <int NW>
+// W4T > 0: the 4-wave uniform-MLP pipeline with W4T tiles per wave and a W4H-tile
+// head (one kernel per shape: a single pipeline per kernel keeps the program
+// argument in SGPRs and the ring in registers)
+template <int NW, int W4T = 0, int W4H = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
                                                                float *__restrict__ act, float *__restrict__ hidden,
                                                                int B, int steps) {
-  fused_body<NW, false>(P, obs, act, hidden, B, steps, DevCtl{});
+  fused_body<NW, false, W4T, W4H>(P, obs, act, hidden, B, steps, DevCtl{});
 }
 
-template <int NW>
+template <int NW, int W4T = 0, int W4H = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(DevProgram P, DevCtl C, float *__restrict__ hidden,
                                                                    int B) {
-  fused_body<NW, true>(P, nullptr, nullptr, hidden, B, 1, C);
+  fused_body<NW, true, W4T, W4H>(P, nullptr, nullptr, hidden, B, 1, C);
 }
 
 // ---------------------------------------------------------------------------
@@ -1373,24 +1689,42 @@ static size_t fused_ctl_lds_bytes(const DevProgram &p, int waves) {
   return fused_lds_bytes(p, waves) + sizeof(float) * ctl_lds_floats(GO2PI_TILE_ROWS, p.in_dim);
 }
 
-template <int NW>
+template <int NW, int W4T = 0, int W4H = 0>
 static hipError_t set_fused_lds(const DevProgram &p) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW, W4T, W4H>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds_bytes(p, NW));
   if (e != hipSuccess) return e;
   const size_t ctl = fused_ctl_lds_bytes(p, NW);
   if (ctl > 160 * 1024) return hipSuccess;  // controller tick unavailable for this width (launch fails loudly)
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW>),
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW, W4T, W4H>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ctl);
+}
+
+// The kernel instantiation for (waves, p.w4_tpw, p.head_fuse): f(kernel tag).
+template <int NW, int W4T, int W4H>
+struct FusedTag {};
+template <class F>
+static void with_fused(const DevProgram &p, int waves, F &&f) {
+  if (waves == 4 && p.w4_tpw) {
+    const bool h2 = p.head_fuse == 2;
+    switch (p.w4_tpw) {
+      case 2: h2 ? f(FusedTag<4, 2, 2>{}) : f(FusedTag<4, 2, 1>{}); return;
+      case 4: h2 ? f(FusedTag<4, 4, 2>{}) : f(FusedTag<4, 4, 1>{}); return;
+      default: f(FusedTag<4, 8, 1>{}); return;  // 8 tiles per wave: one head tile only (engine.cpp)
+    }
+  }
+  switch (waves) {
+    case 4: f(FusedTag<4, 0, 0>{}); return;
+    case 16: f(FusedTag<16, 0, 0>{}); return;
+    default: f(FusedTag<8, 0, 0>{}); return;
+  }
 }
 
 int configure_kernels(const DevProgram &p, int waves) {
   hipError_t e = hipSuccess;
-  switch (waves) {
-    case 4: e = set_fused_lds<4>(p); break;
-    case 16: e = set_fused_lds<16>(p); break;
-    default: e = set_fused_lds<8>(p); break;
-  }
+  with_fused(p, waves, [&](auto tag) {
+    e = [&]<int NW, int T, int H>(FusedTag<NW, T, H>) { return set_fused_lds<NW, T, H>(p); }(tag);
+  });
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
   for (int l = 0; l < p.nl; ++l) gmax = std::max(gmax, (int)gemv_lds_bytes(p, l));
@@ -1405,17 +1739,12 @@ int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float 
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_lds_bytes(p, waves);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  switch (waves) {
-    case 4:
-      hipLaunchKernelGGL(policy_fused_kernel<4>, grid, dim3(256), lds, s, p, obs, act, hidden, batch, steps);
-      break;
-    case 16:
-      hipLaunchKernelGGL(policy_fused_kernel<16>, grid, dim3(1024), lds, s, p, obs, act, hidden, batch, steps);
-      break;
-    default:
-      hipLaunchKernelGGL(policy_fused_kernel<8>, grid, dim3(512), lds, s, p, obs, act, hidden, batch, steps);
-      break;
-  }
+  with_fused(p, waves, [&](auto tag) {
+    [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
+      hipLaunchKernelGGL((policy_fused_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p, obs, act, hidden, batch,
+                         steps);
+    }(tag);
+  });
   return (int)hipGetLastError();
 }
 
@@ -1426,11 +1755,11 @@ int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, f
   const size_t lds = fused_ctl_lds_bytes(p, waves);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  switch (waves) {
-    case 4: hipLaunchKernelGGL(policy_fused_ctl_kernel<4>, grid, dim3(256), lds, s, p, ctl, hidden, batch); break;
-    case 16: hipLaunchKernelGGL(policy_fused_ctl_kernel<16>, grid, dim3(1024), lds, s, p, ctl, hidden, batch); break;
-    default: hipLaunchKernelGGL(policy_fused_ctl_kernel<8>, grid, dim3(512), lds, s, p, ctl, hidden, batch); break;
-  }
+  with_fused(p, waves, [&](auto tag) {
+    [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
+      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p, ctl, hidden, batch);
+    }(tag);
+  });
   return (int)hipGetLastError();
 }
 

@@ -21,7 +21,8 @@ EXPORTS = [
     "go2pi_default_opts", "go2pi_create", "go2pi_create_from_memory", "go2pi_destroy", "go2pi_num_io",
     "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
     "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
-    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_inspect_model", "go2pi_diag_stamps",
+    "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_batched_kernel", "go2pi_inspect_model",
+    "go2pi_diag_stamps",
     "go2pi_last_error", "go2pi_version", "go2pi_ctl_default_params", "go2pi_ctl_set_params",
     "go2pi_ctl_history", "go2pi_controller_step", "go2pi_controller_step_device",
 ]
@@ -119,6 +120,7 @@ def lib():
             "go2pi_hidden_dim": (ctypes.c_int, [P, P]),
             "go2pi_sync": (ctypes.c_int, [P]),
             "go2pi_get_cost": (ctypes.c_int, [P, P]),
+            "go2pi_batched_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_diag_stamps": (ctypes.c_int, [P, P, I64]),
             "go2pi_inspect_model": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_last_error": (ctypes.c_char_p, []),
@@ -194,6 +196,9 @@ class Engine:
         _check(L.go2pi_get_cost(h, ctypes.byref(c)))
         self.cost = {"flops_per_row": c.flops_per_row, "weight_bytes": c.weight_bytes,
                      "io_bytes_per_row": c.io_bytes_per_row, "n_layers": c.n_layers, "has_gru": bool(c.has_gru)}
+        kb = ctypes.create_string_buffer(128)
+        _check(L.go2pi_batched_kernel(h, kb, 128))
+        self.batched_kernel = kb.value.decode()  # e.g. "policy_fused_kernel<4, 8, 1>" (rocprofv3 name)
 
     def _io(self, is_out, k):
         L = lib()

@@ -51,7 +51,7 @@ typedef struct go2pi_opts {
   int64_t max_batch;     /* robots per call capacity (device buffers), default 4096 */
   int32_t use_graph;     /* 1 (default): the small-batch host path replays a captured hipGraph */
   int32_t log_level;     /* OrtLoggingLevel-compatible: 0 VERBOSE … 4 FATAL, default 2 */
-  int32_t waves;         /* waves per workgroup of the batched kernel: 4, 8 or 16 (0 = auto: 8) */
+  int32_t waves;         /* waves per workgroup of the batched kernel: 4, 8 or 16 (0 = auto: 4 for a uniform MLP, else 8) */
   int32_t small_batch;   /* host batches <= this use the GEMV chain (0 = auto: 8; -1 = never) */
   /* Optional fused prologue / epilogue (north_star: obs normalisation, action tanh/clip).
      All OFF by default so act() stays comparable to the shipped graph. */
@@ -118,6 +118,13 @@ typedef struct go2pi_cost {
   int32_t has_gru;
 } go2pi_cost;
 int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
+
+/* Name of the batched kernel instantiation this engine launches for batches
+   above the small-batch paths, e.g. "policy_fused_kernel<4, 8, 1>" (waves per
+   workgroup, tiles per wave of the 4-wave pipeline, head tiles), as rocprofv3
+   reports it. Writes a NUL-terminated string into buf (truncated to cap-1). For
+   profiling tools; no compute. */
+int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap);
 
 /* Parse and lower an ONNX policy WITHOUT touching a device (no compute): writes a
    JSON description (I/O names and shapes, the lowered layer program with
