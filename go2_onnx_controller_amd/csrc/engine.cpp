@@ -78,7 +78,8 @@ struct go2pi_engine {
   bool latency_ok = false;
   unsigned long long *d_gran = nullptr;  // [nl-1][gstride] {tag, value} granules
   int gstride = 0;
-  unsigned *h_err = nullptr, *m_err = nullptr;    // host-mapped timeout word
+  unsigned *h_err = nullptr, *m_err = nullptr;    // host-mapped error words: [0] batch-1 hand-off, [64] batched
+                                                   // kernel layer hand-off (each on its own cache line)
   unsigned *h_done = nullptr, *m_done = nullptr;  // host-mapped completion word (own cache line)
   bool done_ok = false;                            // final layer is one tile: WG 0 signals completion
   go2pi::DevProgram *d_prog = nullptr;             // device copy of prog (latency kernel argument)
@@ -156,6 +157,10 @@ struct go2pi_engine {
     if (h_err && __atomic_load_n(h_err, __ATOMIC_ACQUIRE)) {
       __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
       throw HipError("batch-1 kernel hand-off timed out (workgroups not co-resident?)", GO2PI_E_DEVICE);
+    }
+    if (h_err && __atomic_load_n(h_err + 64, __ATOMIC_ACQUIRE)) {
+      __atomic_store_n(h_err + 64, 0u, __ATOMIC_RELEASE);
+      throw HipError("batched kernel: a layer hand-off between waves timed out (outputs invalid)", GO2PI_E_DEVICE);
     }
   }
 
@@ -436,14 +441,15 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     for (int l = 0; l < p.nl; ++l) kmax = std::max(kmax, p.L[l].K_pad);
     e.latency_ok = !m.has_gru && kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
                    !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
+    hip_check(hipHostMalloc((void **)&e.h_err, 512, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    std::memset(e.h_err, 0, 512);
+    hip_check(hipHostGetDevicePointer((void **)&e.m_err, e.h_err, 0), "hipHostGetDevicePointer");
+    p.err = e.m_err + 64;  // batched kernel hand-off timeouts
     if (e.latency_ok) {
       e.gstride = GO2PI_SMALL_MAXB * maxw;
       const size_t ng = (size_t)std::max(1, p.nl - 1) * e.gstride;
       e.d_gran = e.dalloc<unsigned long long>(ng);
       hip_check(hipMemset(e.d_gran, 0, ng * sizeof(unsigned long long)), "hipMemset");
-      hip_check(hipHostMalloc((void **)&e.h_err, 256, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
-      std::memset(e.h_err, 0, 256);
-      hip_check(hipHostGetDevicePointer((void **)&e.m_err, e.h_err, 0), "hipHostGetDevicePointer");
       e.h_done = e.h_err + 32;  // 128 B apart: its own cache line
       e.m_done = e.m_err + 32;
       e.done_ok = p.L[p.nl - 1].N_pad == 16;
@@ -637,6 +643,7 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
       e->enqueue(e->d_obs, e->d_act, batch, e->stream);
       hip_check(hipMemcpyAsync(act, e->d_act, out_b, hipMemcpyDeviceToHost, e->stream), "hipMemcpyAsync D2H");
       hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      e->check_handoff();
     }
     return GO2PI_OK;
   });
@@ -649,6 +656,7 @@ int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int6
     if (batch == 0) return GO2PI_OK;
     if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
+    e->check_handoff();  // a failure of an earlier asynchronous launch surfaces here (or at go2pi_sync)
     e->enqueue(obs_dev, act_dev, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
   });
@@ -894,6 +902,7 @@ int go2pi_sync(go2pi_engine *e) {
     check_engine(e);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    e->check_handoff();
     return GO2PI_OK;
   });
 }

@@ -965,108 +965,234 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
 }
 
 // ---------------------------------------------------------------------------
-// Uniform-MLP pipeline at one wave per SIMD (4 waves per workgroup, engine
-// option waves = 4): every hidden layer is exactly one tile group per wave
-// (N_pad = 64 * TPW) and the final layer is fused as the head (HT tiles). The
-// weight-fragment register ring of dense_acc_ring runs ACROSS layer
-// boundaries: the tail of layer l's contraction issues layer l + 1's first RD
-// chunks, and layer 0's are issued before the barrier that completes the
-// observation tile, so no layer starts on an L2 round trip. Per-accumulator k
-// order, epilogue and head are those of the generic path (bitwise the same
-// results as dense_group at 4 waves).
+// Uniform-MLP pipeline at one wave per SIMD (4 waves per workgroup; the engine
+// selects it for policies whose hidden layers are all 64 * TPW wide, TPW = 2, 4
+// or 8, with the final layer fused as the head). Wave w owns output tiles
+// [t0, t0 + TPW) of EVERY hidden layer, t0 = w * TPW, over the full K.
+//
+//  * Weight stream: a 4-slot register ring of MFMA A-operand fragments (slot =
+//    consumption index k & 3) filled RD chunks ahead by buffer loads, one per 4
+//    MFMAs. It runs across layer boundaries: the tail of layer l issues layer
+//    l + 1's first RD chunks, layer 0's go out before the observation barrier.
+//  * Register hand-off: the k-chunks of layer l + 1 that a wave produced itself
+//    (chunks t0 .. t0 + TPW - 1: its own output tiles of layer l) are consumed
+//    FIRST and straight from registers: the epilogue value of tile t0 + i (one
+//    float4 per lane = the MFMA B operand for that chunk) feeds chunk i, and the
+//    epilogue of tile i + 1 is interleaved with chunk i's MFMAs (sched_group
+//    pattern). Each tile also goes to LDS for the other waves. The remaining
+//    chunks are read from LDS in rotated order (t0 + k mod C) after ONE wait on
+//    the other waves' per-layer flags (LDS words) — no workgroup barrier between
+//    layers, and the epilogue runs beside the MFMA pipe instead of in front of it.
+//  * WAR safety of the two LDS activation buffers: a wave writes layer l + 1's
+//    tiles into the buffer layer l read only after it has seen every wave's
+//    layer-l flag, which each wave sets after it finished reading that buffer
+//    (its layer l contraction).
+// Numerics: every accumulator is an fp32 fma chain over its K in a fixed
+// per-output order (own chunks first, then rotated): identical for every robot
+// row, so sharded and unsharded runs stay bitwise equal; the order differs from
+// the generic body's, which the tolerance-based parity tests cover.
 
-template <int TPW, int RD>
-__device__ __forceinline__ void w4_prefetch(const DevLayer &L, int t0, int lane, float4 (&f)[4][TPW]) {
-  const WStream ws(L.w);
-  const int csb = (L.N_pad >> 4) * 1024;
+// one chunk (16 k) of MFMAs for the wave's TPW tiles: A = ring slot S, B = b
+// (4 k-steps in its components); LOAD: after every 4th MFMA the next fragment of
+// the chunk RD ahead goes into slot (S + RD) & 3 at byte offset soff of ws. PIN:
+// sched_barrier around each load (the LDS phase); otherwise the caller's
+// sched_group pattern places it (the own phase).
+template <int TPW, int S, int RD, bool LOAD, bool PIN>
+__device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b, const WStream &ws,
+                                         const int (&vo)[TPW], int soff) {
 #pragma unroll
-  for (int d = 0; d < RD; ++d)
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) f[d][i] = ws.ld(((t0 + i) * 64 + lane) * 16, d * csb);
-}
-
-// Contraction of layer L for tiles [t0, t0 + TPW) over all C = K_pad / 16 chunks.
-// On entry f holds chunks 0 .. RD - 1 in slots 0 .. RD - 1 (chunk c lives in slot
-// c & 3; C % 4 == 0). NEXT: the tail issues NL's chunks 0 .. RD - 1 into the
-// slots the loop has freed, which are slots 0 .. RD - 1 again.
-template <int TPW, int RD, bool NEXT>
-__device__ __forceinline__ void w4_contract(const float *X, int xs, const DevLayer &L, const DevLayer &NL, int t0,
-                                            int lane, f32x4 (&acc)[TPW], float4 (&f)[4][TPW]) {
-  const int C = L.K_pad >> 4;
-  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  const WStream ws(L.w), wn(NL.w);
-  const int csb = (L.N_pad >> 4) * 1024, csn = (NL.N_pad >> 4) * 1024;
-  int vo[TPW];  // same tiles of L and NL: per-lane byte offset in chunk 0
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
-  float4 a[2];
-  a[0] = *reinterpret_cast<const float4 *>(xrow);
-  auto group = [&](int c0, auto tail_k) {
-    constexpr bool TAIL = decltype(tail_k)::value;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = c0 + u;
-      if (!(TAIL && u == 3)) a[(u + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
-      const bool OWN = !(TAIL && u + RD >= 4);  // chunk c + RD of this layer exists
-      const bool LOAD = OWN || NEXT;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-          acc[i] = mfma4(f4c(f[u][i], j), f4c(a[u & 1], j), acc[i]);
-          const int s = j * TPW + i;
-          if (LOAD && (s & 3) == 3) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (OWN) f[(u + RD) & 3][s >> 2] = ws.ld(vo[s >> 2], (c + RD) * csb);
-            else f[(u + RD) & 3][s >> 2] = wn.ld(vo[s >> 2], (u + RD - 4) * csn);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-  };
-  int c0 = 0;
-  for (; c0 + 4 < C; c0 += 4) group(c0, std::false_type{});
-  group(c0, std::true_type{});
-}
-
-// Epilogue of a pipeline hidden layer: every tile is valid (no bounds checks),
-// all TPW activated float4s are computed before the first LDS store, and alpha
-// comes in a register, so the stores go out back to back with no scalar-load
-// wait between them (lgkmcnt counts LDS and scalar loads together).
-template <int TPW, bool KEEP>
-__device__ __forceinline__ void w4_store(int act, float alpha, const f32x4 (&acc)[TPW], const float4 (&bv)[TPW],
-                                         float *Y, int ys, int t0, int lane, float4 (&keep)[TPW]) {
-  float *yrow = Y + (lane & 15) * ys + t0 * 16 + ((lane >> 4) << 2);
-  with_act(act, [&](auto act_k) {
-    constexpr int ACT = decltype(act_k)::value;
-    float4 v[TPW];
+  for (int j = 0; j < 4; ++j) {
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      v[i].x = act_t<ACT>(alpha, acc[i][0] + bv[i].x);
-      v[i].y = act_t<ACT>(alpha, acc[i][1] + bv[i].y);
-      v[i].z = act_t<ACT>(alpha, acc[i][2] + bv[i].z);
-      v[i].w = act_t<ACT>(alpha, acc[i][3] + bv[i].w);
+      acc[i] = mfma4(f4c(f[S][i], j), f4c(b, j), acc[i]);
+      const int s = j * TPW + i;
+      if (LOAD && (s & 3) == 3) {
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+        f[(S + RD) & 3][s >> 2] = ws.ld(vo[s >> 2], soff);
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
-    if constexpr (KEEP) {
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) keep[i] = v[i];
-    }
-  });
+  }
 }
 
-// One policy step of the pipeline (the observation tile is being staged into X).
+// bias + activation of one 16 x 16 tile (output-major: one float4 per lane)
+template <int ACT>
+__device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const float4 &bv) {
+  float4 v;
+  v.x = act_t<ACT>(alpha, acc[0] + bv.x);
+  v.y = act_t<ACT>(alpha, acc[1] + bv.y);
+  v.z = act_t<ACT>(alpha, acc[2] + bv.z);
+  v.w = act_t<ACT>(alpha, acc[3] + bv.w);
+  return v;
+}
+
+// One own-phase chunk: the MFMAs of chunk I (B operand b = the epilogue value of
+// the previous layer's tile t0 + I, from registers) with the epilogue of tile
+// I + 1 (accumulator pa, bias pb) woven between them when NEXT. The epilogue is
+// cut into short dependent stages, one after each MFMA from the 4th on (per
+// element: bias add; for Elu also x*log2(e), exp2, alpha*(e-1), select), each
+// pinned by sched_barrier, so its VALU issues in the MFMA pipe's shadow and every
+// dependent stage sits >= 4 MFMAs after its producer. Other activations compute
+// the whole epilogue behind the chunk's MFMAs. Results are bitwise those of
+// w4_epi (the same operations in the same order per element).
+template <int TPW, int S, int RD, int ACT, bool NEXT>
+__device__ __forceinline__ void w4_own_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b,
+                                             const WStream &ws, const int (&vo)[TPW], int soff, const f32x4 &pa,
+                                             const float4 &pb, float alpha, float4 &vn) {
+  constexpr int NM = 4 * TPW;                // MFMAs in the chunk
+  constexpr int NSTG = ACT == 1 ? 5 : 1;    // stages per element
+  constexpr int NS = 4 * NSTG;              // stage slots (4 elements)
+  constexpr int FIRST = NM >= 8 ? 3 : 0;    // first MFMA followed by a stage
+  constexpr int SLOTS = NM - FIRST;
+  constexpr int PER = (NS + SLOTS - 1) / SLOTS;  // stages after each MFMA
+  float t[4], u[4];
+  auto stage = [&](auto q_k) {
+    constexpr int Q = decltype(q_k)::value;  // stage index: element Q % 4, step Q / 4
+    constexpr int E = Q & 3, ST = Q >> 2;
+    // (the empty asm on each stage's result keeps the stages where they are put:
+    // otherwise the SLP vectorizer merges the four elements' stages into packed
+    // ops at the first position)
+    if constexpr (ACT == 1) {
+      if constexpr (ST == 0) {
+        t[E] = pa[E] + f4c(pb, E);
+        asm volatile("" : "+v"(t[E]));
+      } else if constexpr (ST == 1) {
+        u[E] = t[E] * 1.4426950408889634f;
+        asm volatile("" : "+v"(u[E]));
+      } else if constexpr (ST == 2) {
+        u[E] = __builtin_amdgcn_exp2f(u[E]);
+        asm volatile("" : "+v"(u[E]));
+      } else if constexpr (ST == 3) {
+        u[E] = alpha * (u[E] - 1.f);
+        asm volatile("" : "+v"(u[E]));
+      } else {
+        float r = t[E] > 0.f ? t[E] : u[E];
+        asm volatile("" : "+v"(r));
+        if constexpr (E == 0) vn.x = r;
+        else if constexpr (E == 1) vn.y = r;
+        else if constexpr (E == 2) vn.z = r;
+        else vn.w = r;
+      }
+    } else {
+      const float r = act_t<ACT>(alpha, pa[E] + f4c(pb, E));
+      if constexpr (E == 0) vn.x = r;
+      else if constexpr (E == 1) vn.y = r;
+      else if constexpr (E == 2) vn.z = r;
+      else vn.w = r;
+    }
+  };
+  auto stages_after = [&](auto m_k) {
+    constexpr int M = decltype(m_k)::value;
+    if constexpr (NEXT && M >= FIRST) {
+      constexpr int Q0 = (M - FIRST) * PER;
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((Q0 + P < NS ? stage(std::integral_constant<int, (Q0 + P < NS ? Q0 + P : 0)>{}) : void()), ...);
+      }(std::make_integer_sequence<int, PER>{});
+    }
+  };
+  [&]<int... M>(std::integer_sequence<int, M...>) {
+    (([&] {
+       constexpr int J = M / TPW, I = M % TPW;
+       acc[I] = mfma4(f4c(f[S][I], J), f4c(b, J), acc[I]);
+       if constexpr (NEXT) asm volatile("" : "+a"(acc[I]));  // the MFMA stays in its slot of the weave
+       if constexpr ((M & 3) == 3) f[(S + RD) & 3][M >> 2] = ws.ld(vo[M >> 2], soff);
+       stages_after(std::integral_constant<int, M>{});
+       __builtin_amdgcn_sched_barrier(0);
+     }()),
+     ...);
+  }(std::make_integer_sequence<int, NM>{});
+}
+
+// Chunks k in [k0, C) of a layer from the LDS activation rows X, chunk
+// c = (kb + k) mod C, ring slots by k (k0 % 4 == K0S; C % 4 == 0). Groups of 4
+// chunks, the last one NT chunks long ((C - k0) % 4 == NT % 4). NEXT: past the
+// layer's own chunks the ring loads NL's chunks (kbn + d) mod Cn, d < RD (NL's
+// consumption order).
+template <int TPW, int RD, int K0S, int NT, bool NEXT>
+__device__ __forceinline__ void w4_lds_phase(const float *X, int xs, int lane, int C, int kb, int k0,
+                                             const WStream &ws, int csb, const WStream &wn, int csn, int kbn, int Cn,
+                                             const int (&vo)[TPW], f32x4 (&acc)[TPW], float4 (&f)[4][TPW]) {
+  static_assert((K0S == 0 || K0S == 2) && (NT == 2 || NT == 4) && RD <= NT, "phase shape");
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  auto chunk_of = [&](int k) {
+    const int c = kb + k;
+    return c >= C ? c - C : c;
+  };
+  auto next_of = [&](int d) {
+    const int c = kbn + d;
+    return c >= Cn ? c - Cn : c;
+  };
+  float4 a[2];
+  a[0] = *reinterpret_cast<const float4 *>(xrow + chunk_of(k0) * 16);
+  // one group of 4 chunks from k = g (slots K0S .. K0S + 3, mod 4); TAIL: the last
+  auto group = [&](int g, auto tail_k) {
+    constexpr bool TAIL = decltype(tail_k)::value;
+    auto step = [&](auto u_k) {
+      constexpr int U = decltype(u_k)::value;
+      constexpr int S = (K0S + U) & 3;
+      constexpr int N = TAIL ? NT : 4;  // chunks in this group
+      if constexpr (U < N) {
+        const int k = g + U;
+        if (U + 1 < N || !TAIL) a[(U + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + chunk_of(k + 1) * 16);
+        constexpr bool OWN = !(TAIL && U + RD >= N);  // chunk k + RD is this layer's
+        if constexpr (OWN)
+          w4_chunk<TPW, S, RD, true, true>(acc, f, a[U & 1], ws, vo, chunk_of(k + RD) * csb);
+        else if constexpr (NEXT)
+          w4_chunk<TPW, S, RD, true, true>(acc, f, a[U & 1], wn, vo, next_of(U + RD - N) * csn);
+        else
+          w4_chunk<TPW, S, RD, false, true>(acc, f, a[U & 1], ws, vo, 0);
+      }
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+  };
+  int g = k0;
+  for (; g + NT < C; g += 4) group(g, std::false_type{});
+  group(g, std::true_type{});
+}
+
+// Bounded wait until every OTHER wave has published epoch ep (an LDS word per
+// wave). A protocol failure must not hang the GPU: past the bound the kernel
+// reports through P.err (the engine raises it at the next sync) and goes on.
+__device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int lane, unsigned *err) {
+  for (int it = 0;; ++it) {
+    const int f = lane < 4 && lane != wave ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP)
+                                           : ep;
+    if (__ballot(f < ep) == 0ull) break;
+    if (it == (1 << 22)) {  // ~ seconds
+      if (lane == 0 && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // the LDS reads of the other waves' tiles stay after the wait
+}
+
+// One policy step of the pipeline (the observation tile is being staged into bufA).
 template <int TPW, int HT, bool CTL>
-__device__ __forceinline__ void w4_step(const DevProgram &P, float *X, float *Y, int S, f32x4 *scratch, int wave,
-                                        int lane, float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
-                                        const CtlLds &CL, int step) {
+__device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float *bufB, int S, f32x4 *scratch,
+                                        int *flags, int &ep, int wave, int lane, float *ac, const CtlView cv,
+                                        int row0, int B, const DevCtl &ctl, const CtlLds &CL, int step) {
   constexpr int RD = GO2PI_RING_RD;
+  constexpr int CH = 4 * TPW;  // k-chunks of every layer after the first
   const int t0 = wave * TPW;
+  const int nh = P.nl - 1;  // hidden layers; P.L[nh] is the fused head
+  int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
   float4 f[4][TPW];
-  w4_prefetch<TPW, RD>(P.L[0], t0, lane, f);
-  __syncthreads();  // the observation tile is complete in X
+  {
+    const WStream w0(P.L[0].w);
+    const int cs0 = (P.L[0].N_pad >> 4) * 1024;
+#pragma unroll
+    for (int d = 0; d < RD; ++d)
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) f[d][i] = w0.ld(vo[i], d * cs0);
+  }
+  __syncthreads();  // the observation tile is complete in bufA
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1076,77 +1202,152 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *X, float *Y,
     if (threadIdx.x == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
 #endif
   }
-  const int nh = P.nl - 1;  // hidden layers; P.L[nh] is the fused head
-  for (int l = 0; l < nh; ++l) {
-    const DevLayer &L = P.L[l];
-    const int T = L.N_pad >> 4;
-    const int act = L.act;
-    const float alpha = L.alpha;
-    float4 bv[TPW];
-    load_bias<TPW>(bv, L.bias, t0, T, lane);
-    f32x4 acc[TPW];
+  // the head's fragments (final layer, fused): fetched before the last hidden layer's LDS phase
+  float4 hw[HT][TPW];
+  auto load_head = [&](const DevLayer &) {
+    const DevLayer &HL = P.L[nh];
+    const float4 *HW = reinterpret_cast<const float4 *>(HL.w);
+    const int HTL = HL.N_pad >> 4;
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef GO2PI_DIAG_CLOCK
-    unsigned long long *st = (P.stamps && l == 1 && lane == 0)
-                                 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave
-                                 : nullptr;
-    if (st) st[0] = __builtin_amdgcn_s_memtime();
+    for (int h = 0; h < HT; ++h)
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)(t0 + i) * HTL + h) * 64 + lane];
+  };
+  if (nh == 1) load_head(P.L[0]);
+  // layer 0: the observation tile, natural chunk order; the tail fetches layer 1's own chunks
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bv[TPW];
+  load_bias<TPW>(bv, P.L[0].bias, t0, P.L[0].N_pad >> 4, lane);
+  {
+    const DevLayer &L = P.L[0];
+    const DevLayer &NL = P.L[nh > 1 ? 1 : 0];
+    const WStream ws(L.w), wn(NL.w);
+    if (nh > 1)
+      w4_lds_phase<TPW, RD, 0, 4, true>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn,
+                                     (NL.N_pad >> 4) * 1024, t0, CH, vo, acc, f);
+    else
+      w4_lds_phase<TPW, RD, 0, 4, false>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn, 0, 0, 1, vo,
+                                      acc, f);
+  }
+#ifdef GO2PI_DIAG_CLOCK  // pipeline stamps: 6 + l = wave 0 done with hidden layer l, 6 + nh = head barrier;
+                         // 16 + 3w + min(l, 2) = wave w done with hidden layer l
+  if (lane == 0 && P.stamps && step == 0) {
+    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave] = __builtin_amdgcn_s_memtime();
+    if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6] = __builtin_amdgcn_s_memtime();
+  }
 #endif
-    if (l + 1 < nh) {
-      w4_contract<TPW, RD, true>(X, S, L, P.L[l + 1], t0, lane, acc, f);
-#ifdef GO2PI_DIAG_CLOCK
-      if (st) st[1] = __builtin_amdgcn_s_memtime();
+  float *Y = bufB;  // where the previous layer's activations go
+  for (int l = 1; l < nh; ++l) {
+    const DevLayer &PL = P.L[l - 1], &L = P.L[l];
+    const bool more = l + 1 < nh;
+    const DevLayer &NL = P.L[more ? l + 1 : l];
+    const WStream ws(L.w), wn(NL.w);
+    const int csb = (L.N_pad >> 4) * 1024, csn = (NL.N_pad >> 4) * 1024;
+    f32x4 accn[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) accn[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bvn[TPW];
+    load_bias<TPW>(bvn, L.bias, t0, L.N_pad >> 4, lane);
+    float *yrow = Y + (lane & 15) * S + t0 * 16 + ((lane >> 4) << 2);
+    const float alpha = PL.alpha;
+    // own phase: layer l-1's epilogue of tile i+1 beside layer l's MFMAs of chunk t0+i
+    with_act(PL.act, [&](auto act_k) {
+      constexpr int ACT = decltype(act_k)::value;
+      float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
+      *reinterpret_cast<float4 *>(yrow) = v;
+      auto own = [&](auto i_k) {
+        constexpr int I = decltype(i_k)::value;
+        const int cl = (t0 + I + RD) & (CH - 1);  // chunk loaded into slot (I + RD) & 3
+        constexpr int IN = I + 1 < TPW ? I + 1 : I;
+        float4 vn = v;
+        w4_own_chunk<TPW, (I & 3), RD, ACT, (I + 1 < TPW)>(accn, f, v, ws, vo, cl * csb, acc[IN], bv[IN], alpha,
+                                                           vn);
+        if constexpr (I + 1 < TPW) {
+          v = vn;
+          *reinterpret_cast<float4 *>(yrow + (I + 1) * 16) = v;
+        }
+      };
+      own(std::integral_constant<int, 0>{});
+      if constexpr (TPW > 1) own(std::integral_constant<int, 1>{});
+      if constexpr (TPW > 2) {
+        own(std::integral_constant<int, 2>{});
+        own(std::integral_constant<int, 3>{});
+      }
+      if constexpr (TPW > 4) {
+        own(std::integral_constant<int, 4>{});
+        own(std::integral_constant<int, 5>{});
+        own(std::integral_constant<int, 6>{});
+        own(std::integral_constant<int, 7>{});
+      }
+    });
+#ifdef GO2PI_DIAG_CLOCK  // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
+    unsigned long long *sub =
+        (lane == 0 && P.stamps && step == 0 && l == 1) ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 28 + 3 * wave
+                                                        : nullptr;
+    if (sub) sub[0] = __builtin_amdgcn_s_memtime();
 #endif
-      float4 none[TPW];
-      w4_store<TPW, false>(act, alpha, acc, bv, Y, S, t0, lane, none);
+    // publish this wave's layer l-1 tiles, wait for the other waves'
+    ++ep;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
+    if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    w4_wait(flags, wave, ep, lane, P.err);
 #ifdef GO2PI_DIAG_CLOCK
-      if (st) st[2] = __builtin_amdgcn_s_memtime();
+    if (sub) sub[1] = __builtin_amdgcn_s_memtime();
 #endif
+    // LDS phase: the other waves' chunks, rotated order from t0 + TPW
+    constexpr int NT = (3 * TPW) % 4 ? (3 * TPW) % 4 : 4;  // chunks in the LDS phase's last group
+    if (more) {
+      w4_lds_phase<TPW, RD, (TPW & 3), NT, true>(Y, S, lane, CH, t0, TPW, ws, csb, wn, csn, t0, CH, vo, accn, f);
     } else {
-      const DevLayer &HL = P.L[nh];
-      const float4 *HW = reinterpret_cast<const float4 *>(HL.w);
-      const int HTL = HL.N_pad >> 4;
-      float4 hw[HT][TPW];
-#pragma unroll
-      for (int h = 0; h < HT; ++h)
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)(t0 + i) * HTL + h) * 64 + lane];
-      w4_contract<TPW, RD, false>(X, S, L, L, t0, lane, acc, f);
+      load_head(L);  // the head's fragments, behind the last LDS phase
+      w4_lds_phase<TPW, RD, (TPW & 3), NT, false>(Y, S, lane, CH, t0, TPW, ws, csb, wn, csn, 0, 1, vo, accn, f);
+    }
 #ifdef GO2PI_DIAG_CLOCK
-      if (st) st[1] = __builtin_amdgcn_s_memtime();
+    if (sub) sub[2] = __builtin_amdgcn_s_memtime();
 #endif
-      float4 yv[TPW];
-      w4_store<TPW, true>(act, alpha, acc, bv, Y, S, t0, lane, yv);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      acc[i] = accn[i];
+      bv[i] = bvn[i];
+    }
+    Y = Y == bufA ? bufB : bufA;
 #ifdef GO2PI_DIAG_CLOCK
-      if (st) st[2] = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && P.stamps && step == 0 && l < 8) {
+      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave + (l < 3 ? l : 2)] = __builtin_amdgcn_s_memtime();
+      if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
+    }
 #endif
-      f32x4 hacc[HT];
+  }
+  // the last hidden layer's epilogue feeds the head from registers (no LDS copy)
+  {
+    const DevLayer &PL = P.L[nh - 1];
+    f32x4 hacc[HT];
 #pragma unroll
-      for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float alpha = PL.alpha;
+    with_act(PL.act, [&](auto act_k) {
+      constexpr int ACT = decltype(act_k)::value;
 #pragma unroll
-      for (int i = 0; i < TPW; ++i)
+      for (int i = 0; i < TPW; ++i) {
+        const float4 v = w4_epi<ACT>(alpha, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
-          hacc[h] = mfma4(hw[h][i].x, yv[i].x, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].y, yv[i].y, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].z, yv[i].z, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].w, yv[i].w, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].x, v.x, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].y, v.y, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].z, v.z, hacc[h]);
+          hacc[h] = mfma4(hw[h][i].w, v.w, hacc[h]);
         }
+      }
+    });
 #pragma unroll
-      for (int h = 0; h < HT; ++h) scratch[(h * 4 + wave) * 64 + lane] = hacc[h];
-    }
-    __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-    if (threadIdx.x == 0 && P.stamps && step == 0 && l < 8) {
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-      if (l + 1 == nh) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
-    }
-#endif
-    float *t = X;
-    X = Y;
-    Y = t;
+    for (int h = 0; h < HT; ++h) scratch[(h * 4 + wave) * 64 + lane] = hacc[h];
   }
+  __syncthreads();
+#ifdef GO2PI_DIAG_CLOCK
+  if (threadIdx.x == 0 && P.stamps && step == 0 && nh < 9) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + nh] = __builtin_amdgcn_s_memtime();
+#endif
   head_finish<4>(P, P.L[nh], scratch, wave, lane, ac, cv, row0, B);
 }
 
@@ -1262,7 +1463,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     if (step > 0) stage_obs(step);
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
-      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, wave, lane, ac, cv, row0, B, ctl, CL, step);
+      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, flags, ep, wave, lane, ac, cv, row0, B, ctl, CL, step);
       continue;
     }
     __syncthreads();

@@ -60,6 +60,7 @@ struct DevProgram {
   DevGru gru;
   unsigned long long *stamps;  // diagnostics only (GO2PI_DIAG_CLOCK builds): 4 per workgroup
   const float *zero;           // >= 64 zero floats in device memory (source of the padding lanes' loads)
+  unsigned *err;               // host-mapped word: set to 1 when a wave-to-wave layer hand-off times out
   DevLayer L[GO2PI_MAX_LAYERS];
 };
 

@@ -12,7 +12,9 @@ mkdir -p $O
 D=$R/go2_onnx_controller_amd/lib/diag
 WL=${WL:-go2_mlp_512_b4096}
 libof() { if [ "$1" = default ]; then echo $R/go2_onnx_controller_amd/lib/libgo2pi.so; else echo $D/libgo2pi_$1.so; fi; }
+[ "${VARIANTS:-}" = none ] && ROUNDS=skip
 for rnd in ${ROUNDS:-1 2}; do
+  [ "$rnd" = skip ] && break
   for v in ${VARIANTS:-default}; do
     for w in ${WAVES:-8}; do
       GO2PI_LIB=$(libof $v) timeout -k 10 120 python3 $R/bench.py --workload $WL --waves $w --no-cpu --no-latency --no-ctl --steps 400 > $O/b_${v}_w${w}_$rnd.json 2> $O/b_${v}_w${w}_$rnd.err || { echo "bench $v w$w failed"; tail -5 $O/b_${v}_w${w}_$rnd.err; exit 1; }
@@ -24,7 +26,7 @@ export GO2PI_DIAG_STAMPS=1
 for v in ${CLOCKS:-}; do
   for w in ${CLOCK_WAVES:-8}; do
     GO2PI_LIB=$D/libgo2pi_$v.so timeout -k 10 120 python3 $R/tools/clock_probe.py --model ${MODEL:-go2_mlp_512} --waves $w > $O/clock_${v}_w$w.json 2> $O/clock_${v}_w$w.err || { echo "clock $v failed"; tail -5 $O/clock_${v}_w$w.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'])"
+    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'], 'sub', d.get('pipeline_layer1_subphases'))"
   done
 done
 unset GO2PI_DIAG_STAMPS

@@ -68,6 +68,13 @@ def main():
         if np.all(s0 > 0):
             waves_l1[w] = [float(np.median(s0 - st[:, 6])), float(np.median(s1 - st[:, 6])),
                            float(np.median(s2 - st[:, 6])), float(np.median(st[:, 7] - st[:, 6]))]
+    # pipeline builds (4-wave uniform MLP): layer-1 sub-phases per wave, slots 28 + 3w +
+    # {own phase done, flag wait done, LDS phase done}, relative to the wave's layer-0 end (16 + 3w)
+    sub_l1 = {}
+    for w in range(min(args.waves, 4)):
+        a, b, c, z = st[:, 28 + 3 * w], st[:, 29 + 3 * w], st[:, 30 + 3 * w], st[:, 16 + 3 * w]
+        if np.all(a > 0) and np.all(z > 0):
+            sub_l1[w] = [float(np.median(a - z)), float(np.median(b - z)), float(np.median(c - z))]
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
         names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
@@ -87,7 +94,8 @@ def main():
            "wg_start_spread_us": float((st[:, 1].max() - st[:, 1].min()) / 100),
            "wg_end_spread_us": float((st[:, 3].max() - st[:, 3].min()) / 100),
            "phase_cycles_median": phases,
-           "layer1_wave_marks": waves_l1}  # [entry, contraction done, epilogue done, barrier] cycles
+           "layer1_wave_marks": waves_l1,  # [entry, contraction done, epilogue done, barrier] cycles
+           "pipeline_layer1_subphases": sub_l1}
     print(json.dumps(out))
 
 
