@@ -388,6 +388,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       e.waves = 4;
       p.head_fuse = t_last;
       p.w4_tpw = tpw;
+      p.w4_bias = (p.nl - 1) * 64 * tpw;
     }
   }
 

@@ -36,12 +36,23 @@ namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#if defined(GO2PI_DIAG_RD1)
-#define GO2PI_RING_RD 1
+#if defined(GO2PI_DIAG_RD2)
+#define GO2PI_RING_RD 2
 #elif defined(GO2PI_DIAG_RD3)
 #define GO2PI_RING_RD 3
 #else
-#define GO2PI_RING_RD 2  // chunks ahead of the weight-fragment ring at 4 waves per workgroup
+#define GO2PI_RING_RD 1  // chunks ahead of the weight-fragment ring at 4 waves per workgroup (2, 3: slower)
+#endif
+// the 4-wave pipeline's ring depth by tiles per wave: a chunk is 4 * TPW MFMAs
+// (32 cycles each), and a fragment must be issued >= ~1K cycles (an L2 round trip
+// under load) before its MFMA
+#ifndef GO2PI_DIAG_RD2
+#ifndef GO2PI_DIAG_RD3
+#define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? 1 : ((TPW) >= 4 ? 2 : 3))
+#endif
+#endif
+#ifndef GO2PI_W4_RD
+#define GO2PI_W4_RD(TPW) GO2PI_RING_RD
 #endif
 #ifndef GO2PI_WPOL  // weight-fragment load policy: 0 plain, 1 nt, 2 sc1 (L1 bypass)
 #if defined(GO2PI_DIAG_NT)
@@ -424,7 +435,8 @@ struct Handoff {
   // cross-layer prefetch (barrier hand-off only): this wave's first tile
   // group's chunk-0 fragments, loaded before the barrier (prefetch_first)
   float4 pre[4];
-  int npre;  // valid entries of pre (0: none)
+  int npre;       // valid entries of pre (0: none)
+  unsigned *err;  // set to 1 when a poll runs out of its bound (the engine raises it)
 };
 
 // Issue this wave's first weight fragments of layer L (chunk 0 of its first
@@ -456,6 +468,8 @@ __device__ __forceinline__ void handoff_wait(const Handoff &h, int c, int nw, in
       break;
     }
     if ((ok & need) == need) break;
+    if (it == (1 << 20) - 1 && lane == 0 && h.err)  // never silently: outputs of this launch are invalid
+      __hip_atomic_store(h.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");  // the group's A-operand reads stay after the poll
@@ -1094,7 +1108,6 @@ __device__ __forceinline__ void w4_own_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][T
     (([&] {
        constexpr int J = M / TPW, I = M % TPW;
        acc[I] = mfma4(f4c(f[S][I], J), f4c(b, J), acc[I]);
-       if constexpr (NEXT) asm volatile("" : "+a"(acc[I]));  // the MFMA stays in its slot of the weave
        if constexpr ((M & 3) == 3) f[(S + RD) & 3][M >> 2] = ws.ld(vo[M >> 2], soff);
        stages_after(std::integral_constant<int, M>{});
        __builtin_amdgcn_sched_barrier(0);
@@ -1174,11 +1187,18 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
 // One policy step of the pipeline (the observation tile is being staged into bufA).
 template <int TPW, int HT, bool CTL>
 __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float *bufB, int S, f32x4 *scratch,
-                                        int *flags, int &ep, int wave, int lane, float *ac, const CtlView cv,
-                                        int row0, int B, const DevCtl &ctl, const CtlLds &CL, int step) {
-  constexpr int RD = GO2PI_RING_RD;
+                                        int *flags, float *lbias, int &ep, int wave, int lane, float *ac,
+                                        const CtlView cv, int row0, int B, const DevCtl &ctl, const CtlLds &CL,
+                                        int step) {
+  constexpr int RD = GO2PI_W4_RD(TPW);
   constexpr int CH = 4 * TPW;  // k-chunks of every layer after the first
+  // register hand-off between layers for 4 and 8 tiles per wave; at 2 tiles per
+  // wave (a 128-wide policy such as the shipped model) a layer's own phase is too
+  // short to cover the other waves' epilogues, and an epilogue + barrier + natural
+  // chunk order measured faster (9.9 vs 11.0 us per 4096-robot step)
+  constexpr bool HO = TPW >= 4;
   const int t0 = wave * TPW;
+  const int kb1 = HO ? t0 : 0;  // first k-chunk of every layer after the first
   const int nh = P.nl - 1;  // hidden layers; P.L[nh] is the fused head
   int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
 #pragma unroll
@@ -1192,7 +1212,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
 #pragma unroll
       for (int i = 0; i < TPW; ++i) f[d][i] = w0.ld(vo[i], d * cs0);
   }
-  __syncthreads();  // the observation tile is complete in bufA
+  // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
+  // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
+  // weight stream, whose waits would otherwise cover them); the head's bias to registers
+  if (step == 0)
+    for (int l = 0; l < nh; ++l) glds_copy(lbias + l * CH * 16, P.L[l].bias, CH * 16, wave, lane, 4);
+  float4 hbv[1];
+  load_bias<1>(hbv, P.L[nh].bias, wave < HT ? wave : 0, P.L[nh].N_pad >> 4, lane);
+#ifdef GO2PI_DIAG_CLOCK
+  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 42] = __builtin_amdgcn_s_memtime();
+#endif
+  __syncthreads();  // the observation tile is complete in bufA (and the biases in LDS)
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1218,15 +1248,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
   f32x4 acc[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float *brow = lbias + t0 * 16 + ((lane >> 4) << 2);  // this lane's bias float4 of tile t0, layer 0
   float4 bv[TPW];
-  load_bias<TPW>(bv, P.L[0].bias, t0, P.L[0].N_pad >> 4, lane);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) bv[i] = *reinterpret_cast<const float4 *>(brow + i * 16);
   {
     const DevLayer &L = P.L[0];
     const DevLayer &NL = P.L[nh > 1 ? 1 : 0];
     const WStream ws(L.w), wn(NL.w);
     if (nh > 1)
       w4_lds_phase<TPW, RD, 0, 4, true>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn,
-                                     (NL.N_pad >> 4) * 1024, t0, CH, vo, acc, f);
+                                     (NL.N_pad >> 4) * 1024, kb1, CH, vo, acc, f);
     else
       w4_lds_phase<TPW, RD, 0, 4, false>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn, 0, 0, 1, vo,
                                       acc, f);
@@ -1249,10 +1281,24 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
 #pragma unroll
     for (int i = 0; i < TPW; ++i) accn[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 bvn[TPW];
-    load_bias<TPW>(bvn, L.bias, t0, L.N_pad >> 4, lane);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) bvn[i] = *reinterpret_cast<const float4 *>(brow + l * CH * 16 + i * 16);
     float *yrow = Y + (lane & 15) * S + t0 * 16 + ((lane >> 4) << 2);
     const float alpha = PL.alpha;
-    // own phase: layer l-1's epilogue of tile i+1 beside layer l's MFMAs of chunk t0+i
+    // publish this wave's layer l-1 tiles (after its own LDS stores) for the other waves
+    auto publish = [&] {
+      ++ep;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
+      if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#ifdef GO2PI_DIAG_CLOCK  // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
+    unsigned long long *sub =
+        (lane == 0 && P.stamps && step == 0 && l == 1) ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 28 + 3 * wave
+                                                        : nullptr;
+#endif
+#ifdef GO2PI_DIAG_WEAVE
+    // variant (diagnostics): layer l-1's epilogue of tile i+1 woven between layer l's
+    // MFMAs of chunk t0+i (measured slower: the woven VALU stretches the MFMA gaps)
     with_act(PL.act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
       float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
@@ -1269,40 +1315,46 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
           *reinterpret_cast<float4 *>(yrow + (I + 1) * 16) = v;
         }
       };
-      own(std::integral_constant<int, 0>{});
-      if constexpr (TPW > 1) own(std::integral_constant<int, 1>{});
-      if constexpr (TPW > 2) {
-        own(std::integral_constant<int, 2>{});
-        own(std::integral_constant<int, 3>{});
-      }
-      if constexpr (TPW > 4) {
-        own(std::integral_constant<int, 4>{});
-        own(std::integral_constant<int, 5>{});
-        own(std::integral_constant<int, 6>{});
-        own(std::integral_constant<int, 7>{});
+      [&]<int... I>(std::integer_sequence<int, I...>) {
+        (own(std::integral_constant<int, I>{}), ...);
+      }(std::make_integer_sequence<int, TPW>{});
+    });
+    publish();
+#else
+    // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
+    // publish, then layer l's MFMAs over those chunks with the B operand from registers
+    // (!HO: the epilogue to LDS, then a workgroup barrier)
+    with_act(PL.act, [&](auto act_k) {
+      constexpr int ACT = decltype(act_k)::value;
+      float4 v[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
+      if constexpr (HO) {
+        publish();
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (w4_chunk<TPW, (I & 3), RD, true, true>(accn, f, v[I], ws, vo, ((t0 + I + RD) & (CH - 1)) * csb), ...);
+        }(std::make_integer_sequence<int, TPW>{});
       }
     });
-#ifdef GO2PI_DIAG_CLOCK  // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
-    unsigned long long *sub =
-        (lane == 0 && P.stamps && step == 0 && l == 1) ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 28 + 3 * wave
-                                                        : nullptr;
+    if constexpr (!HO) __syncthreads();
+#endif
+#ifdef GO2PI_DIAG_CLOCK
     if (sub) sub[0] = __builtin_amdgcn_s_memtime();
 #endif
-    // publish this wave's layer l-1 tiles, wait for the other waves'
-    ++ep;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
-    if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    w4_wait(flags, wave, ep, lane, P.err);
+    if constexpr (HO) w4_wait(flags, wave, ep, lane, P.err);
 #ifdef GO2PI_DIAG_CLOCK
     if (sub) sub[1] = __builtin_amdgcn_s_memtime();
 #endif
     // LDS phase: the other waves' chunks, rotated order from t0 + TPW
-    constexpr int NT = (3 * TPW) % 4 ? (3 * TPW) % 4 : 4;  // chunks in the LDS phase's last group
+    constexpr int K0 = HO ? TPW : 0;                             // first chunk index of the LDS phase
+    constexpr int NT = (CH - K0) % 4 ? (CH - K0) % 4 : 4;       // chunks in the LDS phase's last group
     if (more) {
-      w4_lds_phase<TPW, RD, (TPW & 3), NT, true>(Y, S, lane, CH, t0, TPW, ws, csb, wn, csn, t0, CH, vo, accn, f);
+      w4_lds_phase<TPW, RD, (K0 & 3), NT, true>(Y, S, lane, CH, kb1, K0, ws, csb, wn, csn, kb1, CH, vo, accn, f);
     } else {
       load_head(L);  // the head's fragments, behind the last LDS phase
-      w4_lds_phase<TPW, RD, (TPW & 3), NT, false>(Y, S, lane, CH, t0, TPW, ws, csb, wn, csn, 0, 1, vo, accn, f);
+      w4_lds_phase<TPW, RD, (K0 & 3), NT, false>(Y, S, lane, CH, kb1, K0, ws, csb, wn, csn, 0, 1, vo, accn, f);
     }
 #ifdef GO2PI_DIAG_CLOCK
     if (sub) sub[2] = __builtin_amdgcn_s_memtime();
@@ -1348,7 +1400,13 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0 && nh < 9) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + nh] = __builtin_amdgcn_s_memtime();
 #endif
-  head_finish<4>(P, P.L[nh], scratch, wave, lane, ac, cv, row0, B);
+  if (wave < HT) {  // head tile `wave`: the four waves' partials in a fixed order, bias, final store
+    f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) hs[0] += scratch[(wave * 4 + w) * 64 + lane];
+    float4 none[1];
+    dense_store<1>(P, P.L[nh], hs, hbv, wave, HT, lane, true, nullptr, 0, ac, cv, row0, B, none);
+  }
 }
 
 // Body of the batched kernel. CTL: controller tick (steps == 1) — the
@@ -1376,11 +1434,24 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // Touch every layer descriptor up front: one burst of scalar loads warms the
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
-  {
+  if constexpr (W4T > 0) {
+    // pipeline: every descriptor slot unconditionally (unused ones are zero), so
+    // the loads carry no data dependence on nl and go out as ONE burst with one
+    // wait instead of a round trip per layer
+    int d = P.nl ^ P.in_dim ^ P.in_pad ^ P.lds_stride ^ (int)(size_t)P.zero ^ (int)(size_t)P.err;
+#pragma unroll
+    for (int l = 0; l < GO2PI_MAX_LAYERS; ++l)
+      d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w ^ (int)(size_t)P.L[l].bias ^
+           __float_as_int(P.L[l].alpha);
+    asm volatile("" ::"s"(d));  // consumes the loads; no side effect
+  } else {
     int d = 0;
     for (int l = 0; l < P.nl; ++l) d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w;
     asm volatile("" ::"s"(d));  // consumes the loads; no side effect
   }
+#ifdef GO2PI_DIAG_CLOCK  // init sub-phases: 40 descriptors warm, 41 observation loads issued, 42 pipeline barrier reached
+  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 40] = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef GO2PI_DIAG_CLOCK
   if (tid == 0 && P.stamps) {
     P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();
@@ -1396,7 +1467,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   int *flags = reinterpret_cast<int *>(after_scratch);
   if (tid < NW) flags[tid] = 0;
   int ep = 0;  // hand-offs published so far (identical in every wave)
-  const CtlLds CL = ctl_lds(after_scratch + GO2PI_FLAG_FLOATS, GO2PI_TILE_ROWS, P.in_dim);
+  // (the pipeline's bias copy sits between the flags and the controller-tick region)
+  float *lbias = after_scratch + GO2PI_FLAG_FLOATS;
+  const CtlLds CL = ctl_lds(lbias + P.w4_bias, GO2PI_TILE_ROWS, P.in_dim);
   CtlView cv{};
   CtlQ cq{};
   if constexpr (CTL) {
@@ -1415,6 +1488,22 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
       ctl_assemble<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
                          ctl.obs + (size_t)row0 * P.in_dim, wave, lane, NW);
+    } else if (W4T > 0 && glds_obs) {
+      // pipeline (in_pad = layer 0's K_pad, a multiple of 64): wave w stages rows
+      // w, w + 4, w + 8, w + 12; per-lane source pointers are formed once, so the
+      // loop carries no scalar reloads between the direct-to-LDS loads
+      const int in_dim = P.in_dim, nch = P.in_pad >> 6;
+      const float *ob = obs + (size_t)step * B * in_dim;
+      const float *zero = P.zero + lane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wave + 4 * i, row = row0 + r;
+        const float *rp = ob + (size_t)row * in_dim + lane;
+        for (int c = 0; c < nch; ++c) {
+          const float *src = (row < B && c * 64 + lane < in_dim) ? rp + c * 64 : zero;
+          __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
+        }
+      }
     } else if (glds_obs) {
       // one direct-to-LDS load per (row, 64-column chunk): the tile's observation
       // loads all in flight together; padding lanes and rows past B read zeros
@@ -1440,7 +1529,10 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // next layer, so they must hold finite values: clear everything the
   // observation does not cover, once.
   stage_obs(0);
-  if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
+#ifdef GO2PI_DIAG_CLOCK
+  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
+#endif
+  if (W4T == 0 && P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tail4 = (S - P.in_pad) >> 2;
     for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
@@ -1451,7 +1543,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
     for (int e = tid; e < n4; e += NT) l4[e] = z;
   }
-  if (P.has_gru) {
+  if (W4T == 0 && P.has_gru) {
     __syncthreads();  // bufH zero fill above before the hidden rows land
     for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
       const int r = e / H, k = e - r * H, row = row0 + r;
@@ -1463,7 +1555,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     if (step > 0) stage_obs(step);
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
-      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, flags, ep, wave, lane, ac, cv, row0, B, ctl, CL, step);
+      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, ac, cv, row0, B, ctl, CL,
+                             step);
       continue;
     }
     __syncthreads();
@@ -1499,7 +1592,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         __syncthreads();
         head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, cv, row0, B);
 #ifdef GO2PI_DIAG_CLOCK
-        if (tid == 0 && P.stamps && step == 0 && l < 9) {
+        if (tid == 0 && P.stamps && step == 0 && l < 8) {  // slots 6..14 (15 is the controller tick's)
           P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
           P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
         }
@@ -1522,6 +1615,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         ++ep;
         handoff_publish(flags, wave, lane, ep);
         hin = Handoff{flags, ep, (T + NW - 1) / NW};
+        hin.err = P.err;
       } else {
         hin = Handoff{nullptr, 0, 1};
 #ifdef GO2PI_DIAG_PREFETCH  // variant (diagnostics): measured slower, see DESIGN §4.1
@@ -1530,7 +1624,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         __syncthreads();
       }
 #ifdef GO2PI_DIAG_CLOCK
-      if (tid == 0 && P.stamps && step == 0 && l < 10)
+      if (tid == 0 && P.stamps && step == 0 && l < 9)  // slots 6..14 (15 is the controller tick's)
         P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
 #endif
       float *t = X;
@@ -1879,7 +1973,8 @@ size_t fused_lds_bytes(const DevProgram &p, int waves) {
   // activation buffers + per-wave partial-sum scratch (head fusion: up to 2 tiles)
   // + the layer hand-off flags
   return sizeof(float) * (size_t)(2 + p.has_gru) * GO2PI_TILE_ROWS * p.lds_stride +
-         sizeof(f32x4) * 64 * waves * (p.head_fuse > 1 ? p.head_fuse : 1) + sizeof(float) * GO2PI_FLAG_FLOATS;
+         sizeof(f32x4) * 64 * waves * (p.head_fuse > 1 ? p.head_fuse : 1) + sizeof(float) * GO2PI_FLAG_FLOATS +
+         sizeof(float) * p.w4_bias;
 }
 
 size_t gemv_lds_bytes(const DevProgram &p, int layer) {

@@ -132,6 +132,8 @@ def lib():
             "go2pi_controller_step_device": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64, P]),
         }
         for name, (res, args) in sig.items():
+            if name == "go2pi_batched_kernel" and not hasattr(L, name) and os.environ.get("GO2PI_LIB"):
+                continue  # an older diagnostics build (A/B tooling): the name query is optional there
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -196,9 +198,11 @@ class Engine:
         _check(L.go2pi_get_cost(h, ctypes.byref(c)))
         self.cost = {"flops_per_row": c.flops_per_row, "weight_bytes": c.weight_bytes,
                      "io_bytes_per_row": c.io_bytes_per_row, "n_layers": c.n_layers, "has_gru": bool(c.has_gru)}
-        kb = ctypes.create_string_buffer(128)
-        _check(L.go2pi_batched_kernel(h, kb, 128))
-        self.batched_kernel = kb.value.decode()  # e.g. "policy_fused_kernel<4, 8, 1>" (rocprofv3 name)
+        self.batched_kernel = "unknown"
+        if hasattr(L, "go2pi_batched_kernel") and L.go2pi_batched_kernel.argtypes:
+            kb = ctypes.create_string_buffer(128)
+            _check(L.go2pi_batched_kernel(h, kb, 128))
+            self.batched_kernel = kb.value.decode()  # e.g. "policy_fused_kernel<4, 8, 1>" (rocprofv3 name)
 
     def _io(self, is_out, k):
         L = lib()

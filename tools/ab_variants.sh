@@ -17,8 +17,11 @@ for rnd in ${ROUNDS:-1 2}; do
   [ "$rnd" = skip ] && break
   for v in ${VARIANTS:-default}; do
     for w in ${WAVES:-8}; do
-      GO2PI_LIB=$(libof $v) timeout -k 10 120 python3 $R/bench.py --workload $WL --waves $w --no-cpu --no-latency --no-ctl --steps 400 > $O/b_${v}_w${w}_$rnd.json 2> $O/b_${v}_w${w}_$rnd.err || { echo "bench $v w$w failed"; tail -5 $O/b_${v}_w${w}_$rnd.err; exit 1; }
-      python3 -c "import json;d=json.load(open('$O/b_${v}_w${w}_$rnd.json'));print('round $rnd $v waves $w', d['kernel_us'], d['roofline']['frac'])"
+      for wl in ${WLS:-$WL}; do
+        f=$O/b_${v}_w${w}_${wl}_$rnd
+        GO2PI_LIB=$(libof $v) timeout -k 10 180 python3 $R/bench.py --workload $wl --waves $w --no-cpu --no-latency --steps 400 $([ -z "$CTLLEG" ] && echo --no-ctl) > $f.json 2> $f.err || { echo "bench $v w$w $wl failed"; tail -5 $f.err; exit 1; }
+        python3 -c "import json;d=json.load(open('$f.json'));print('round $rnd $v waves $w $wl', d['kernel_us'], d['roofline']['frac'], d.get('controller_tick', ''))"
+      done
     done
   done
 done
@@ -26,7 +29,7 @@ export GO2PI_DIAG_STAMPS=1
 for v in ${CLOCKS:-}; do
   for w in ${CLOCK_WAVES:-8}; do
     GO2PI_LIB=$D/libgo2pi_$v.so timeout -k 10 120 python3 $R/tools/clock_probe.py --model ${MODEL:-go2_mlp_512} --waves $w > $O/clock_${v}_w$w.json 2> $O/clock_${v}_w$w.err || { echo "clock $v failed"; tail -5 $O/clock_${v}_w$w.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'], 'sub', d.get('pipeline_layer1_subphases'))"
+    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'], 'sub', d.get('pipeline_layer1_subphases'), 'init', d.get('init_subphases'))"
   done
 done
 unset GO2PI_DIAG_STAMPS

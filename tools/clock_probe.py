@@ -75,6 +75,11 @@ def main():
         a, b, c, z = st[:, 28 + 3 * w], st[:, 29 + 3 * w], st[:, 30 + 3 * w], st[:, 16 + 3 * w]
         if np.all(a > 0) and np.all(z > 0):
             sub_l1[w] = [float(np.median(a - z)), float(np.median(b - z)), float(np.median(c - z))]
+    init_sub = {}
+    if np.all(st[:, 40] > 0):  # init sub-phases (slots 40-42) relative to the workgroup start
+        for k, nm in ((40, "descriptors"), (41, "obs_issued"), (42, "barrier_reached")):
+            if np.all(st[:, k] > 0):
+                init_sub[nm] = float(np.median(st[:, k] - st[:, 0]))
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
         names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
@@ -95,7 +100,7 @@ def main():
            "wg_end_spread_us": float((st[:, 3].max() - st[:, 3].min()) / 100),
            "phase_cycles_median": phases,
            "layer1_wave_marks": waves_l1,  # [entry, contraction done, epilogue done, barrier] cycles
-           "pipeline_layer1_subphases": sub_l1}
+           "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub}
     print(json.dumps(out))
 
 
