@@ -389,6 +389,12 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       p.head_fuse = t_last;
       p.w4_tpw = tpw;
       p.w4_bias = (p.nl - 1) * 64 * tpw;
+      std::vector<float> pack(p.w4_bias);
+      for (int l = 0; l + 1 < p.nl; ++l)
+        hip_check(hipMemcpy(pack.data() + (size_t)l * 64 * tpw, p.L[l].bias, sizeof(float) * 64 * tpw,
+                            hipMemcpyDeviceToHost),
+                  "hipMemcpy");
+      p.w4_bpack = e.upload(pack);
     }
   }
 

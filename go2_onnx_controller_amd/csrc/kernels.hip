@@ -1215,8 +1215,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
   // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
   // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
   // weight stream, whose waits would otherwise cover them); the head's bias to registers
-  if (step == 0)
-    for (int l = 0; l < nh; ++l) glds_copy(lbias + l * CH * 16, P.L[l].bias, CH * 16, wave, lane, 4);
+  if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
   float4 hbv[1];
   load_bias<1>(hbv, P.L[nh].bias, wave < HT ? wave : 0, P.L[nh].N_pad >> 4, lane);
 #ifdef GO2PI_DIAG_CLOCK
@@ -1435,15 +1434,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
   if constexpr (W4T > 0) {
-    // pipeline: every descriptor slot unconditionally (unused ones are zero), so
-    // the loads carry no data dependence on nl and go out as ONE burst with one
-    // wait instead of a round trip per layer
-    int d = P.nl ^ P.in_dim ^ P.in_pad ^ P.lds_stride ^ (int)(size_t)P.zero ^ (int)(size_t)P.err;
-#pragma unroll
-    for (int l = 0; l < GO2PI_MAX_LAYERS; ++l)
-      d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w ^ (int)(size_t)P.L[l].bias ^
-           __float_as_int(P.L[l].alpha);
-    asm volatile("" ::"s"(d));  // consumes the loads; no side effect
+    // pipeline: no warm-up (holding every descriptor in SGPRs spilled them to VGPR
+    // lanes; the fields are read where needed and hit the scalar cache after the
+    // first layer)
   } else {
     int d = 0;
     for (int l = 0; l < P.nl; ++l) d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w;

@@ -50,6 +50,7 @@ struct DevProgram {
   int zero_fill;   // 1: clear LDS activation buffers at kernel start (padded columns never written)
   int w4_tpw;      // >0: 4-wave uniform-MLP pipeline (kernels.hip, w4_step), tiles per wave of every hidden layer
   int w4_bias;     // pipeline: LDS floats holding every hidden layer's bias (sum of their N_pad), else 0
+  const float *w4_bpack;  // pipeline: those biases packed back to back in device memory (one LDS-DMA stream)
   // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
   const float *pre_sub;
   const float *pre_div;
