@@ -82,7 +82,7 @@ struct go2pi_engine {
                                                    // kernel layer hand-off (each on its own cache line)
   unsigned *h_done = nullptr, *m_done = nullptr;  // host-mapped completion word (own cache line)
   bool done_ok = false;                            // final layer is one tile: WG 0 signals completion
-  go2pi::DevProgram *d_prog = nullptr;             // device copy of prog (latency kernel argument)
+  go2pi::DevProgram *d_prog = nullptr;             // device copy of prog (what every kernel reads)
   unsigned epoch = 1, last_epoch = 0;
   // controller tick (go2pi_controller_step*)
   int ctl_hist = 0;                        // kHistory when the policy's I/O is a Go2 controller's, else 0
@@ -171,7 +171,8 @@ struct go2pi_engine {
       hip_check(go2pi::launch_latency_ctl(prog, d_prog, c, (int)batch, e0, d_gran, gstride, m_err, done, s),
                 "controller latency launch");
     } else {
-      hip_check(go2pi::launch_policy_fused_ctl(prog, waves, c, d_hidden, (int)batch, s), "controller fused launch");
+      hip_check(go2pi::launch_policy_fused_ctl(prog, d_prog, waves, c, d_hidden, (int)batch, s),
+                "controller fused launch");
     }
   }
 
@@ -192,7 +193,7 @@ struct go2pi_engine {
         xs = ys;
       }
     } else {
-      hip_check(go2pi::launch_policy_fused(prog, waves, obs, act, d_hidden, (int)batch, 1, s), "fused launch");
+      hip_check(go2pi::launch_policy_fused(prog, d_prog, waves, obs, act, d_hidden, (int)batch, 1, s), "fused launch");
     }
   }
 
@@ -681,7 +682,8 @@ int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_
       throw ApiError("sequence too large", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    hip_check(go2pi::launch_policy_fused(e->prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch, (int)steps, s),
+    hip_check(go2pi::launch_policy_fused(e->prog, e->d_prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch,
+                                         (int)steps, s),
               "fused sequence launch");
     return GO2PI_OK;
   });

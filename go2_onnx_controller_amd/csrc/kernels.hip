@@ -1674,17 +1674,21 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 // W4T > 0: the 4-wave uniform-MLP pipeline with W4T tiles per wave and a W4H-tile
 // head (one kernel per shape: a single pipeline per kernel keeps the program
 // argument in SGPRs and the ring in registers)
+// The program is read from its device-memory copy (L2-resident across launches)
+// rather than passed by value: a by-value kernarg is a fresh copy per launch, and
+// every cache line of it a workgroup first touches is a memory round trip.
 template <int NW, int W4T = 0, int W4H = 0>
-__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(DevProgram P, const float *__restrict__ obs,
+__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram *__restrict__ Pd,
+                                                               const float *__restrict__ obs,
                                                                float *__restrict__ act, float *__restrict__ hidden,
                                                                int B, int steps) {
-  fused_body<NW, false, W4T, W4H>(P, obs, act, hidden, B, steps, DevCtl{});
+  fused_body<NW, false, W4T, W4H>(*Pd, obs, act, hidden, B, steps, DevCtl{});
 }
 
 template <int NW, int W4T = 0, int W4H = 0>
-__global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(DevProgram P, DevCtl C, float *__restrict__ hidden,
-                                                                   int B) {
-  fused_body<NW, true, W4T, W4H>(P, nullptr, nullptr, hidden, B, 1, C);
+__global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
+                                                                   float *__restrict__ hidden, int B) {
+  fused_body<NW, true, W4T, W4H>(*Pd, nullptr, nullptr, hidden, B, 1, C);
 }
 
 // ---------------------------------------------------------------------------
@@ -2054,23 +2058,23 @@ int configure_kernels(const DevProgram &p, int waves) {
   return (int)e;
 }
 
-int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float *act, float *hidden, int batch,
-                        int steps, void *stream) {
+int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves, const float *obs, float *act,
+                        float *hidden, int batch, int steps, void *stream) {
   if (batch <= 0 || steps <= 0) return 0;
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_lds_bytes(p, waves);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   with_fused(p, waves, [&](auto tag) {
     [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
-      hipLaunchKernelGGL((policy_fused_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p, obs, act, hidden, batch,
-                         steps);
+      hipLaunchKernelGGL((policy_fused_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p_dev, obs, act, hidden,
+                         batch, steps);
     }(tag);
   });
   return (int)hipGetLastError();
 }
 
-int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, float *hidden, int batch,
-                            void *stream) {
+int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int waves, const DevCtl &ctl,
+                            float *hidden, int batch, void *stream) {
   if (batch <= 0) return 0;
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_ctl_lds_bytes(p, waves);
@@ -2078,7 +2082,8 @@ int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, f
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   with_fused(p, waves, [&](auto tag) {
     [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
-      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p, ctl, hidden, batch);
+      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p_dev, ctl, hidden,
+                         batch);
     }(tag);
   });
   return (int)hipGetLastError();

@@ -101,8 +101,9 @@ struct DevCtl {  // per call (kernel argument)
 
 // Host-side launchers (kernels.hip). All launches are asynchronous on `stream`.
 // Return a hipError_t as int.
-int launch_policy_fused(const DevProgram &p, int waves, const float *obs, float *act, float *hidden, int batch,
-                        int steps, void *stream);
+// p: host copy (grid, LDS size, kernel choice); p_dev: its device-memory copy (the kernel reads that)
+int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves, const float *obs, float *act,
+                        float *hidden, int batch, int steps, void *stream);
 size_t fused_lds_bytes(const DevProgram &p, int waves);
 int launch_gemv_layer(const DevProgram &p, int layer, const float *x, int x_stride, float *y, int y_stride,
                       int batch, void *stream);
@@ -119,8 +120,8 @@ int launch_latency(const DevProgram &p, const DevProgram *p_dev, const float *ob
 int latency_grid(const DevProgram &p);
 // Controller tick variants of the two launchers above (steps = 1; ctl.obs / ctl.action
 // replace obs / act). The latency variant needs the final layer to be one tile.
-int launch_policy_fused_ctl(const DevProgram &p, int waves, const DevCtl &ctl, float *hidden, int batch,
-                            void *stream);
+int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int waves, const DevCtl &ctl,
+                            float *hidden, int batch, void *stream);
 int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, int batch, unsigned epoch0,
                        unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream);
 

@@ -19,7 +19,7 @@ for rnd in ${ROUNDS:-1 2}; do
     for w in ${WAVES:-8}; do
       for wl in ${WLS:-$WL}; do
         f=$O/b_${v}_w${w}_${wl}_$rnd
-        GO2PI_LIB=$(libof $v) timeout -k 10 180 python3 $R/bench.py --workload $wl --waves $w --no-cpu --no-latency --steps 400 $([ -z "$CTLLEG" ] && echo --no-ctl) > $f.json 2> $f.err || { echo "bench $v w$w $wl failed"; tail -5 $f.err; exit 1; }
+        GO2PI_LIB=$(libof $v) timeout -k 10 180 python3 $R/bench.py --workload $wl --waves $w --no-cpu --no-latency --steps ${STEPS:-400} $([ -z "$CTLLEG" ] && echo --no-ctl) > $f.json 2> $f.err || { echo "bench $v w$w $wl failed"; tail -5 $f.err; exit 1; }
         python3 -c "import json;d=json.load(open('$f.json'));print('round $rnd $v waves $w $wl', d['kernel_us'], d['roofline']['frac'], d.get('controller_tick', ''))"
       done
     done
