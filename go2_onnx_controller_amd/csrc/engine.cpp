@@ -375,12 +375,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     const int t_last = p.L[p.nl - 1].N_pad / 16, t_prev = p.L[p.nl - 2].N_pad / 16;
     if (t_last <= 2 && t_prev >= e.waves) p.head_fuse = t_last;
   }
-  // 4-wave uniform-MLP pipeline (kernels.hip, w4_step): no GRU, a fused head, and
+  // 4-wave uniform-MLP pipeline (kernels.hip, w4_step): a fused head, and
   // every hidden layer exactly one group of 2, 4 or 8 tiles per wave. It is the
   // default (waves = 0) wherever it applies: measured faster than the generic
   // 8-wave body; otherwise waves = 0 means 8.
-  if ((e.opts.waves == 0 || e.opts.waves == 4) && p.nl >= 2 && !m.has_gru && !std::getenv("GO2PI_NO_HEAD_FUSE") &&
-      !std::getenv("GO2PI_NO_W4")) {  // env: A/B diagnostics only
+  // (a GRU policy runs its cell first and hands h' to the pipeline as layer 0's input)
+  if ((e.opts.waves == 0 || e.opts.waves == 4) && p.nl >= 2 && (!m.has_gru || m.gru.H % 64 == 0) &&
+      !std::getenv("GO2PI_NO_HEAD_FUSE") && !std::getenv("GO2PI_NO_W4")) {  // env: A/B diagnostics only
     const int t_last = p.L[p.nl - 1].N_pad / 16;
     const int tpw = p.L[0].N_pad / 64;
     bool uniform = (tpw == 2 || tpw == 4 || tpw == 8) && t_last <= (tpw == 8 ? 1 : 2);

@@ -185,6 +185,12 @@ __device__ __forceinline__ float ctl_gravity(const float *st, float v0, float v1
 // the next __syncthreads() (its fence waits vmcnt(0)).
 typedef __attribute__((address_space(1))) void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
+// Before the barrier that hands LDS-DMA'd bytes to OTHER waves, each issuing wave
+// waits for its own direct-to-LDS loads: the compiler's barrier fence does not
+// count them (MI355X_MICROARCH.md §Two waves per SIMD, item 7: nothing orders a
+// ds_read behind a pending LDS-DMA except the issuing wave's covering vmcnt).
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ void glds_copy(float *dst, const float *src, int n, int wave, int lane, int nw) {
   for (int base = wave * 64; base < n; base += nw * 64) {
     const int i = min(base + lane, n - 1);
@@ -888,7 +894,8 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
   const float4 *W = reinterpret_cast<const float4 *>(G.w);
   const int col = lane & 15, r0 = (lane >> 4) << 2;
   f32x4 z[GT], r[GT], nx[GT], nh[GT];
-  const float4 *wp[GT];
+  const WStream ws(W);
+  int vo[GT];  // per-lane byte offset of tile t_first + i's z fragment in chunk 0 (r: +1 KiB, n: +2 KiB)
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
     const int j = (t_first + i) * 16 + col;
@@ -897,9 +904,9 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
     r[i] = f32x4{br, br, br, br};
     nx[i] = f32x4{bx, bx, bx, bx};
     nh[i] = f32x4{bh, bh, bh, bh};
-    wp[i] = W + (size_t)(t_first + i) * 192 + lane;
+    vo[i] = ((t_first + i) * 192 + lane) * 16;
   }
-  const int cs = (G.H >> 4) * 192;  // chunk-major: [chunk][tile][gate][lane]
+  const int csb = (G.H >> 4) * 192 * 16;  // bytes per chunk, chunk-major: [chunk][tile][gate][lane]
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
   // One stream over the concatenated [x | h] chunks, scheduled like dense_acc:
@@ -908,9 +915,9 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
   float4 cz[GT], cr[GT], chh[GT];
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
-    cz[i] = wp[i][0];
-    cr[i] = wp[i][64];
-    chh[i] = wp[i][128];
+    cz[i] = ws.ld(vo[i], 0);
+    cr[i] = ws.ld(vo[i] + 1024, 0);
+    chh[i] = ws.ld(vo[i] + 2048, 0);
   }
   auto step = [&](int c, const float4 &a, f32x4 (&third)[GT], int cn) {
     float4 nz[GT], nr[GT], nh3[GT];
@@ -931,7 +938,7 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
           if ((s & 3) == 3) {
             const int q = s >> 2, ti = q / 3, gi = q % 3;
             __builtin_amdgcn_sched_barrier(0);
-            const float4 f = wp[ti][cn * cs + 64 * gi];
+            const float4 f = ws.ld(vo[ti] + 1024 * gi, cn * csb);
             if (gi == 0) nz[ti] = f;
             else if (gi == 1) nr[ti] = f;
             else nh3[ti] = f;
@@ -948,21 +955,21 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
       z[i] = mfma4(a.z, cz[i].z, z[i]);
       z[i] = mfma4(a.w, cz[i].w, z[i]);
       __builtin_amdgcn_sched_barrier(0);
-      nz[i] = wp[i][cn * cs];
+      nz[i] = ws.ld(vo[i], cn * csb);
       __builtin_amdgcn_sched_barrier(0);
       r[i] = mfma4(a.x, cr[i].x, r[i]);
       r[i] = mfma4(a.y, cr[i].y, r[i]);
       r[i] = mfma4(a.z, cr[i].z, r[i]);
       r[i] = mfma4(a.w, cr[i].w, r[i]);
       __builtin_amdgcn_sched_barrier(0);
-      nr[i] = wp[i][cn * cs + 64];
+      nr[i] = ws.ld(vo[i] + 1024, cn * csb);
       __builtin_amdgcn_sched_barrier(0);
       third[i] = mfma4(a.x, chh[i].x, third[i]);
       third[i] = mfma4(a.y, chh[i].y, third[i]);
       third[i] = mfma4(a.z, chh[i].z, third[i]);
       third[i] = mfma4(a.w, chh[i].w, third[i]);
       __builtin_amdgcn_sched_barrier(0);
-      nh3[i] = wp[i][cn * cs + 128];
+      nh3[i] = ws.ld(vo[i] + 2048, cn * csb);
       __builtin_amdgcn_sched_barrier(0);
     }
 #endif
@@ -1039,18 +1046,29 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
 // the chunk RD ahead goes into slot (S + RD) & 3 at byte offset soff of ws. PIN:
 // sched_barrier around each load (the LDS phase); otherwise the caller's
 // sched_group pattern places it (the own phase).
+// Load spacing: one fragment load after every LSP-th MFMA, so the chunk's TPW
+// loads are issued over its first LSP * TPW MFMAs (the earlier they go out, the
+// longer the last tile's fragment has before its MFMA in the next chunk).
+#if defined(GO2PI_DIAG_LSP1)
+#define GO2PI_W4_LSP 1
+#elif defined(GO2PI_DIAG_LSP4)
+#define GO2PI_W4_LSP 4
+#elif !defined(GO2PI_W4_LSP)
+#define GO2PI_W4_LSP 2
+#endif
 template <int TPW, int S, int RD, bool LOAD, bool PIN>
 __device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b, const WStream &ws,
                                          const int (&vo)[TPW], int soff) {
+  constexpr int LSP = GO2PI_W4_LSP;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       acc[i] = mfma4(f4c(f[S][i], j), f4c(b, j), acc[i]);
       const int s = j * TPW + i;
-      if (LOAD && (s & 3) == 3) {
+      if (LOAD && s % LSP == LSP - 1 && s / LSP < TPW) {
         if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-        f[(S + RD) & 3][s >> 2] = ws.ld(vo[s >> 2], soff);
+        f[(S + RD) & 3][s / LSP] = ws.ld(vo[s / LSP], soff);
         if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -1213,8 +1231,10 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
 }
 
 // One policy step of the pipeline (the observation tile is being staged into bufA).
+// X0: layer 0's input rows (the observation tile, or a GRU's h'); Y0: the other
+// activation buffer (layer 0's outputs)
 template <int TPW, int HT, bool CTL>
-__device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float *bufB, int S, f32x4 *scratch,
+__device__ __forceinline__ void w4_step(const DevProgram &P, float *X0, float *Y0, int S, f32x4 *scratch,
                                         int *flags, float *lbias, int &ep, int wave, int lane, float *ac,
                                         const CtlView cv, int row0, int B, const DevCtl &ctl, const CtlLds &CL,
                                         int step) {
@@ -1249,7 +1269,8 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 42] = __builtin_amdgcn_s_memtime();
 #endif
-  __syncthreads();  // the observation tile is complete in bufA (and the biases in LDS)
+  lds_dma_wait();   // the observation and bias tiles (this wave's direct-to-LDS loads)
+  __syncthreads();  // layer 0's input rows are complete in X0 (and the biases in LDS)
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1284,10 +1305,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
     const DevLayer &NL = P.L[nh > 1 ? 1 : 0];
     const WStream ws(L.w), wn(NL.w);
     if (nh > 1)
-      w4_lds_phase<TPW, RD, 0, 4, true>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn,
+      w4_lds_phase<TPW, RD, 0, 4, true>(X0, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn,
                                      (NL.N_pad >> 4) * 1024, kb1, CH, vo, acc, f);
     else
-      w4_lds_phase<TPW, RD, 0, 4, false>(bufA, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn, 0, 0, 1, vo,
+      w4_lds_phase<TPW, RD, 0, 4, false>(X0, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn, 0, 0, 1, vo,
                                       acc, f);
   }
 #ifdef GO2PI_DIAG_CLOCK  // pipeline stamps: 6 + l = wave 0 done with hidden layer l, 6 + nh = head barrier;
@@ -1297,7 +1318,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
     if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6] = __builtin_amdgcn_s_memtime();
   }
 #endif
-  float *Y = bufB;  // where the previous layer's activations go
+  float *Y = Y0;  // where the previous layer's activations go
   for (int l = 1; l < nh; ++l) {
     const DevLayer &PL = P.L[l - 1], &L = P.L[l];
     const bool more = l + 1 < nh;
@@ -1391,7 +1412,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *bufA, float 
       acc[i] = accn[i];
       bv[i] = bvn[i];
     }
-    Y = Y == bufA ? bufB : bufA;
+    Y = Y == X0 ? Y0 : X0;
 #ifdef GO2PI_DIAG_CLOCK
     if (lane == 0 && P.stamps && step == 0 && l < 8) {
       P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave + (l < 3 ? l : 2)] = __builtin_amdgcn_s_memtime();
@@ -1497,6 +1518,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     cq = ctl_q(ctl);
     cv = ctl_view(ctl, CL, row0);
     ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
+    lds_dma_wait();
     __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
     if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 5] = __builtin_amdgcn_s_memtime();
@@ -1514,10 +1536,11 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         ctl_assemble<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
                            ctl.obs + (size_t)row0 * P.in_dim, wave, lane, NW);
     } else if (W4T > 0 && glds_obs) {
-      // pipeline (in_pad = layer 0's K_pad, a multiple of 64): wave w stages rows
-      // w, w + 4, w + 8, w + 12; per-lane source pointers are formed once, so the
-      // loop carries no scalar reloads between the direct-to-LDS loads
-      const int in_dim = P.in_dim, nch = P.in_pad >> 6;
+      // pipeline: wave w stages rows w, w + 4, w + 8, w + 12 in whole 64-column
+      // chunks (in_pad is a GRU's input width, not always a multiple of 64);
+      // per-lane source pointers are formed once, so the loop carries no scalar
+      // reloads between the direct-to-LDS loads
+      const int in_dim = P.in_dim, nch = (P.in_pad + 63) >> 6;
       const float *ob = obs + (size_t)step * B * in_dim;
       const float *zero = P.zero + lane;
 #pragma unroll
@@ -1557,7 +1580,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 #ifdef GO2PI_DIAG_CLOCK
   if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
 #endif
-  if (W4T == 0 && P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
+  if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tail4 = (S - P.in_pad) >> 2;
     for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
@@ -1568,7 +1591,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
     for (int e = tid; e < n4; e += NT) l4[e] = z;
   }
-  if (W4T == 0 && P.has_gru) {
+  if (P.has_gru) {
     __syncthreads();  // bufH zero fill above before the hidden rows land
     for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
       const int r = e / H, k = e - r * H, row = row0 + r;
@@ -1580,10 +1603,31 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     if (step > 0) stage_obs(step);
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
-      w4_step<W4T, W4H, CTL>(P, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, ac, cv, row0, B, ctl, CL,
+      float *X0 = bufA, *Y0 = bufB;
+      if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
+        lds_dma_wait();
+        __syncthreads();  // x in bufA, the hidden rows in bufH
+        gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
+        __syncthreads();
+        for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+          const int r = e / H, k = e - r * H;
+          bufH[r * S + k] = bufB[r * S + k];  // read again only in the next step, after w4_step's barriers
+        }
+        X0 = bufB;
+        Y0 = bufA;
+#ifdef GO2PI_DIAG_GRUDBG
+        __syncthreads();
+        if (blockIdx.x == 0 && tid < 2)
+          printf("tid %d x %g %g %g h0 %g %g h1 %g %g %g S %d H %d in_pad %d has_gru %d\n", tid, bufA[tid * S],
+                 bufA[tid * S + 1], bufA[tid * S + 47], bufH[tid * S], bufH[tid * S + 255], bufB[tid * S],
+                 bufB[tid * S + 1], bufB[tid * S + 255], S, H, P.in_pad, P.has_gru);
+#endif
+      }
+      w4_step<W4T, W4H, CTL>(P, X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv, row0, B, ctl, CL,
                              step);
       continue;
     }
+    lds_dma_wait();  // the observation tile's direct-to-LDS loads
     __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
     if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
@@ -1846,7 +1890,10 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
   if constexpr (CTL) {
     cq = ctl_q(ctl);
     cv = ctl_view(ctl, CL, 0);
-    if (g < (P.L[0].N_pad >> 4)) ctl_lds_load(CL, ctl, 0, B, P.in_dim, tid, wave, lane, LAT_WAVES);  // layer-0 WGs
+    if (g < (P.L[0].N_pad >> 4)) {  // layer-0 WGs
+      ctl_lds_load(CL, ctl, 0, B, P.in_dim, tid, wave, lane, LAT_WAVES);
+      lds_dma_wait();  // (the assembly reads the image after this workgroup's next barrier)
+    }
   }
   for (int l = 0; l < P.nl; ++l) {
     const DevLayer &L = P.L[l];
