@@ -238,7 +238,7 @@ void pack_dense(const go2pi::Dense &d, bool last, std::vector<float> &w, std::ve
 // GRU fragments: [Ht][Cx + Ch][gate z,r,h][lane] float4 over the concatenated
 // [x (I_pad) | h (H)] axis; x chunks carry W, h chunks carry R.
 void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
-  I_pad = ceil16(g.I);
+  I_pad = ceil64(g.I);  // whole 4-chunk groups of x (the pipelined cell's ring runs on them)
   const int H = g.H, Ht = H / 16, Cx = I_pad / 16, Ch = H / 16, Cc = Cx + Ch;
   w.assign((size_t)Ht * Cc * 3 * 64 * 4, 0.f);
   for (int t = 0; t < Ht; ++t)

@@ -1230,6 +1230,113 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
   asm volatile("" ::: "memory");  // the LDS reads of the other waves' tiles stay after the wait
 }
 
+// GRU cell as the pipeline's front stage (one wave per SIMD): wave w owns hidden
+// tiles [w * GT, (w + 1) * GT) (H = 64 * GT) over the concatenated [x | h] chunks
+// (Cx = I_pad / 16 and Ch = H / 16, both multiples of 4: the engine pads I to 64).
+// The same register ring and buffer-load stream as the dense layers (RD = 1,
+// loads every 2 MFMAs), B operand one chunk ahead from LDS, output-major
+// accumulators (the gate fragment is the A operand): lane l holds units
+// 16t + 4(l >> 4) + e of robot l & 15, so the old h and the new h' move as one
+// float4 per tile. Gate math as gru_group (ONNX GRU, linear_before_reset = 1).
+// h' goes to Y rows and to hn (registers) for the caller.
+template <int GT>
+__device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
+                                       int lane, float4 (&hn)[GT]) {
+  constexpr int NF = 3 * GT;  // gate fragments per chunk
+  constexpr int NM = 4 * NF;  // MFMAs per chunk
+  const int Cx = G.I_pad >> 4, Ch = G.H >> 4;
+  const int t0 = wave * GT, u0 = (lane >> 4) << 2;
+  const WStream ws(G.w);
+  const int csb = Ch * 3 * 1024;  // bytes per chunk (all tiles, three gates)
+  int vo[GT];                     // per-lane byte offset of tile t0 + i's z fragment in chunk 0 (r +1 KiB, n +2 KiB)
+#pragma unroll
+  for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 3 * 64 + lane) * 16;
+  f32x4 z[GT], r[GT], nx[GT], nh[GT];
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t0 + i) * 16 + u0;
+    const float4 bz = *reinterpret_cast<const float4 *>(G.bzr + j);
+    const float4 br = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
+    const float4 bx = *reinterpret_cast<const float4 *>(G.bh + j);
+    const float4 bh = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
+    z[i] = f32x4{bz.x, bz.y, bz.z, bz.w};
+    r[i] = f32x4{br.x, br.y, br.z, br.w};
+    nx[i] = f32x4{bx.x, bx.y, bx.z, bx.w};
+    nh[i] = f32x4{bh.x, bh.y, bh.z, bh.w};
+  }
+  float4 f[4][NF];
+#pragma unroll
+  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
+  const float *xrow = X + (lane & 15) * xs + u0;
+  const float *hrow = Hs + (lane & 15) * xs + u0;
+  float4 a[2];
+  a[0] = *reinterpret_cast<const float4 *>(xrow);
+  // chunk c (slot S = c & 3); XPH: an x chunk (the third gate accumulates n_x, else
+  // n_h); NEXT: chunk c + 1 exists (its B operand and fragments are fetched here)
+  auto chunk = [&](auto s_k, auto xph_k, auto next_k, int c) {
+    constexpr int S = decltype(s_k)::value;
+    constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value;
+    if constexpr (NEXT) {
+      const float *src = c + 1 < Cx ? xrow + (c + 1) * 16 : hrow + (c + 1 - Cx) * 16;
+      a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(src);
+    }
+    const float4 b = a[S & 1];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int jk = m / NF, i = (m % NF) / 3, g = m % 3;
+      const float wv = f4c(f[S][i * 3 + g], jk), bk = f4c(b, jk);
+      if (g == 0) z[i] = mfma4(wv, bk, z[i]);
+      else if (g == 1) r[i] = mfma4(wv, bk, r[i]);
+      else if (XPH) nx[i] = mfma4(wv, bk, nx[i]);
+      else nh[i] = mfma4(wv, bk, nh[i]);
+      if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
+        const int q = m >> 1;
+        __builtin_amdgcn_sched_barrier(0);
+        f[(S + 1) & 3][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, (c + 1) * csb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int c = 0; c < Cx; c += 4) {
+    chunk(I0{}, T_{}, T_{}, c);
+    chunk(I1{}, T_{}, T_{}, c + 1);
+    chunk(I2{}, T_{}, T_{}, c + 2);
+    chunk(I3{}, T_{}, T_{}, c + 3);
+  }
+  int c = Cx;
+  for (; c + 4 < Cx + Ch; c += 4) {
+    chunk(I0{}, F_{}, T_{}, c);
+    chunk(I1{}, F_{}, T_{}, c + 1);
+    chunk(I2{}, F_{}, T_{}, c + 2);
+    chunk(I3{}, F_{}, T_{}, c + 3);
+  }
+  chunk(I0{}, F_{}, T_{}, c);
+  chunk(I1{}, F_{}, T_{}, c + 1);
+  chunk(I2{}, F_{}, T_{}, c + 2);
+  chunk(I3{}, F_{}, F_{}, c + 3);
+  float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const float4 ho = *reinterpret_cast<const float4 *>(hrow + (t0 + i) * 16);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float zg = sigmoid_fast(z[i][e]);
+      const float rg = sigmoid_fast(r[i][e]);
+      const float hv = 2.f * sigmoid_fast(2.f * (nx[i][e] + rg * nh[i][e])) - 1.f;  // tanh, ~1e-7 abs
+      o[e] = (1.f - zg) * hv + zg * f4c(ho, e);
+    }
+    hn[i] = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4 *>(yrow + i * 16) = hn[i];
+  }
+}
+
 // One policy step of the pipeline (the observation tile is being staged into bufA).
 // X0: layer 0's input rows (the observation tile, or a GRU's h'); Y0: the other
 // activation buffer (layer 0's outputs)
@@ -1607,11 +1714,31 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
         lds_dma_wait();
         __syncthreads();  // x in bufA, the hidden rows in bufH
-        gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
-        __syncthreads();
-        for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-          const int r = e / H, k = e - r * H;
-          bufH[r * S + k] = bufB[r * S + k];  // read again only in the next step, after w4_step's barriers
+        auto carry = [&](auto gt_k) {  // the pipelined cell: h' to bufB, registers, and the carry
+          constexpr int GT = decltype(gt_k)::value;
+          float4 hn[GT];
+          w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn);
+          if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's hidden state: once, from registers
+            float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+            for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + i * 16) = hn[i];
+          }
+          __syncthreads();  // every wave has read bufH
+          float *hl = bufH + (lane & 15) * S + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+          for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hl + i * 16) = hn[i];
+        };
+        if (H == 256) {
+          carry(std::integral_constant<int, 4>{});
+        } else if (H == 128) {
+          carry(std::integral_constant<int, 2>{});
+        } else {
+          gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
+          __syncthreads();
+          for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+            const int r = e / H, k = e - r * H;
+            bufH[r * S + k] = bufB[r * S + k];  // read again only in the next step, after w4_step's barriers
+          }
         }
         X0 = bufB;
         Y0 = bufA;
@@ -1701,7 +1828,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       Y = t;
     }
   }
-  if (P.has_gru) {
+  if (P.has_gru && !(W4T > 0 && (H == 256 || H == 128))) {  // (the pipelined cells store it from registers)
     for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
       const int r = e / H, k = e - r * H, row = row0 + r;
       if (row < B) hidden[(size_t)row * H + k] = bufH[r * S + k];
