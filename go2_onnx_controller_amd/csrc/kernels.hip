@@ -1700,9 +1700,21 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   }
   if (P.has_gru) {
     __syncthreads();  // bufH zero fill above before the hidden rows land
-    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-      const int r = e / H, k = e - r * H, row = row0 + r;
-      bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
+    if (W4T > 0 && H % 64 == 0) {
+      // pipeline: the hidden rows by direct-to-LDS loads, in flight with the
+      // observation's (one 64-column chunk per instruction; rows past B read zeros)
+      for (int i = 0; i < 4; ++i) {
+        const int r = wave + 4 * i, row = row0 + r;
+        for (int c = 0; c < (H >> 6); ++c) {
+          const float *src = row < B ? hidden + (size_t)row * H + c * 64 + lane : P.zero + lane;
+          __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufH + r * S + c * 64), 4, 0, 0);
+        }
+      }
+    } else {
+      for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
+        const int r = e / H, k = e - r * H, row = row0 + r;
+        bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
+      }
     }
   }
   for (int step = 0; step < steps; ++step) {
