@@ -129,6 +129,12 @@ MODELS = {
     "ctl_h1": lambda: mlp_model_bytes((49, 64, 64, 12), seed=7),
     "ctl_h3": lambda: mlp_model_bytes((147, 128, 128, 12), seed=8),
     "gru_ctl": lambda: gru_model_bytes(I=98, H=64, head=(128, 12), seed=9),
+    # shapes of the 4-wave pipeline (kernels.hip w4_step): tiles per wave x head tiles
+    "pipe_256_h2": lambda: mlp_model_bytes((40, 256, 256, 20), seed=10),                      # 4 x 2, hand-off
+    "pipe_128_tanh_h2": lambda: mlp_model_bytes((33, 128, 128, 128, 30), seed=11, act="Tanh"),  # 2 x 2, barrier
+    "pipe_512_relu": lambda: mlp_model_bytes((70, 512, 512, 7), seed=12, act="Relu"),         # 8 x 1, K0 = 128
+    "pipe_one_hidden": lambda: mlp_model_bytes((48, 256, 12), seed=13),                       # one hidden layer
+    "gru_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=14),            # 2-tile GRU stage
 }
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -1,0 +1,69 @@
+"""GPU parity of the 4-wave uniform-MLP pipeline (kernels.hip, w4_step / w4_gru)
+in every shape it is instantiated for, against the fp64 oracle and against the
+generic 8-wave body on the same inputs.
+
+Shapes (tiles per wave x head tiles): 8 x 1 with a 128-wide input (two 64-column
+input chunks, register hand-off between layers), 4 x 2 (hand-off, two head
+tiles), 2 x 2 (epilogue + barrier between layers, Tanh), a single hidden layer
+(the head fetched before layer 0), and GRU front stages with H = 256 and 128.
+Batches cover a partial tile, a partial last workgroup and several workgroups.
+Tolerance: 1e-5 absolute against fp64 (the synthetic models' outputs are
+O(0.1-1)); the generic body is held to the same bound, not to bitwise equality,
+because the pipeline consumes each layer's k-chunks in a rotated order.
+"""
+import numpy as np
+import pytest
+
+from conftest import abs_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+SHAPES = {
+    "pipe_512_relu": "policy_fused_kernel<4, 8, 1>",
+    "pipe_256_h2": "policy_fused_kernel<4, 4, 2>",
+    "pipe_128_tanh_h2": "policy_fused_kernel<4, 2, 2>",
+    "pipe_one_hidden": "policy_fused_kernel<4, 4, 1>",
+    "go2_mlp_512": "policy_fused_kernel<4, 8, 1>",
+}
+
+
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_pipeline_shapes(synth_path, name):
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    p = synth_path(name)
+    g = onnx_ref.load(p)
+    in_dim = g.inputs[0][1][1]
+    x = np.random.default_rng(7).standard_normal((300, in_dim)).astype(np.float32)
+    with Engine(p, max_batch=512, small_batch=-1) as e, Engine(p, max_batch=512, waves=8, small_batch=-1) as gen:
+        assert e.batched_kernel == SHAPES[name]
+        assert gen.batched_kernel.startswith("policy_fused_kernel<8, 0, 0>")
+        for B in (1, 16, 17, 300):
+            want = onnx_ref.act(g, x[:B])
+            assert abs_err(e.run(x[:B]), want) <= TOL, (name, B)
+            assert abs_err(gen.run(x[:B]), want) <= TOL, (name, B)
+
+
+@pytest.mark.parametrize("name,kernel", [("go2_gru_256", "policy_fused_kernel<4, 8, 1>"),
+                                         ("gru_128", "policy_fused_kernel<4, 4, 1>")])
+def test_pipeline_gru_ticks(synth_path, name, kernel):
+    """GRU front stage + MLP pipeline over several ticks (hidden state carried by
+    the engine), against the fp64 ONNX GRU oracle, actions and hidden state."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    p = synth_path(name)
+    g = onnx_ref.load(p)
+    I, H = g.inputs[0][1][1], g.inputs[1][1][2]
+    B, T = 37, 4
+    xs = np.random.default_rng(3).standard_normal((T, B, I)).astype(np.float32)
+    h = np.zeros((1, B, H))
+    with Engine(p, max_batch=64, small_batch=-1) as e:
+        assert e.batched_kernel == kernel
+        e.reset_hidden()
+        for t in range(T):
+            r = onnx_ref.run(g, {"observation": xs[t].astype(np.float64), "h_in": h})
+            h = r["h_out"]
+            assert abs_err(e.run(xs[t]), r["action"]) <= TOL, t
+            assert abs_err(e.get_hidden(B), h[0]) <= TOL, t
