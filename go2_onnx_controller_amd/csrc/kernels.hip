@@ -190,6 +190,16 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // count them (MI355X_MICROARCH.md §Two waves per SIMD, item 7: nothing orders a
 // ds_read behind a pending LDS-DMA except the issuing wave's covering vmcnt).
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Workgroup barrier that leaves this wave's N youngest vector-memory ops in flight
+// (weight fragments prefetched for after the barrier); __syncthreads()'s fence
+// would wait for all of them. Everything older — the LDS-DMA the barrier publishes
+// — has landed: loads return in issue order. The caller keeps exactly N loads
+// between the DMA and this barrier (compiler barriers on both sides).
+template <int N>
+__device__ __forceinline__ void wg_barrier_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 __device__ __forceinline__ void glds_copy(float *dst, const float *src, int n, int wave, int lane, int nw) {
   for (int base = wave * 64; base < n; base += nw * 64) {
@@ -1238,10 +1248,17 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
 // accumulators (the gate fragment is the A operand): lane l holds units
 // 16t + 4(l >> 4) + e of robot l & 15, so the old h and the new h' move as one
 // float4 per tile. Gate math as gru_group (ONNX GRU, linear_before_reset = 1).
-// h' goes to Y rows and to hn (registers) for the caller.
+// h' goes to Y rows and to hn (registers) for the caller. The caller has issued
+// the direct-to-LDS loads of x and h; this stage issues its first chunk's
+// fragments, waits for everything OLDER than them (the LDS-DMA), then barriers,
+// so the fragment latency overlaps the staging. Gate biases are added after the
+// contraction (accumulators start at zero), so their loads wait nowhere.
 template <int GT>
 __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
-                                       int lane, float4 (&hn)[GT]) {
+                                       int lane, float4 (&hn)[GT], unsigned long long *st = nullptr) {
+#ifdef GO2PI_DIAG_CLOCK  // GRU stage marks (wave 0): 43 entry, 44 contraction done, 45 epilogue done
+  if (st && wave == 0 && lane == 0) st[43] = __builtin_amdgcn_s_memtime();
+#endif
   constexpr int NF = 3 * GT;  // gate fragments per chunk
   constexpr int NM = 4 * NF;  // MFMAs per chunk
   const int Cx = G.I_pad >> 4, Ch = G.H >> 4;
@@ -1251,34 +1268,36 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
   int vo[GT];                     // per-lane byte offset of tile t0 + i's z fragment in chunk 0 (r +1 KiB, n +2 KiB)
 #pragma unroll
   for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 3 * 64 + lane) * 16;
+  float4 f[4][NF];
+  asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
+#pragma unroll
+  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
+  wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
   f32x4 z[GT], r[GT], nx[GT], nh[GT];
+  float4 bz[GT], br[GT], bx[GT], bh[GT];
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
     const int j = (t0 + i) * 16 + u0;
-    const float4 bz = *reinterpret_cast<const float4 *>(G.bzr + j);
-    const float4 br = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
-    const float4 bx = *reinterpret_cast<const float4 *>(G.bh + j);
-    const float4 bh = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
-    z[i] = f32x4{bz.x, bz.y, bz.z, bz.w};
-    r[i] = f32x4{br.x, br.y, br.z, br.w};
-    nx[i] = f32x4{bx.x, bx.y, bx.z, bx.w};
-    nh[i] = f32x4{bh.x, bh.y, bh.z, bh.w};
+    bz[i] = *reinterpret_cast<const float4 *>(G.bzr + j);
+    br[i] = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
+    bx[i] = *reinterpret_cast<const float4 *>(G.bh + j);
+    bh[i] = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
+    z[i] = r[i] = nx[i] = nh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  float4 f[4][NF];
-#pragma unroll
-  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
   const float *xrow = X + (lane & 15) * xs + u0;
   const float *hrow = Hs + (lane & 15) * xs + u0;
   float4 a[2];
   a[0] = *reinterpret_cast<const float4 *>(xrow);
   // chunk c (slot S = c & 3); XPH: an x chunk (the third gate accumulates n_x, else
-  // n_h); NEXT: chunk c + 1 exists (its B operand and fragments are fetched here)
-  auto chunk = [&](auto s_k, auto xph_k, auto next_k, int c) {
+  // n_h); NEXT: chunk c + 1 exists (its B operand and fragments are fetched here);
+  // NX: chunk c + 1 is an x chunk (else an h chunk). One fixed source row per
+  // instantiation keeps the B-operand read a single ds_read_b128.
+  auto chunk = [&](auto s_k, auto xph_k, auto next_k, auto nx_k, int c) {
     constexpr int S = decltype(s_k)::value;
-    constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value;
+    constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
     if constexpr (NEXT) {
-      const float *src = c + 1 < Cx ? xrow + (c + 1) * 16 : hrow + (c + 1 - Cx) * 16;
-      a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(src);
+      if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
+      else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (c + 1 - Cx) * 16);
     }
     const float4 b = a[S & 1];
 #pragma unroll
@@ -1303,23 +1322,30 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  for (int c = 0; c < Cx; c += 4) {
-    chunk(I0{}, T_{}, T_{}, c);
-    chunk(I1{}, T_{}, T_{}, c + 1);
-    chunk(I2{}, T_{}, T_{}, c + 2);
-    chunk(I3{}, T_{}, T_{}, c + 3);
+  int c = 0;
+  for (; c + 4 < Cx; c += 4) {
+    chunk(I0{}, T_{}, T_{}, T_{}, c);
+    chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
+    chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
+    chunk(I3{}, T_{}, T_{}, T_{}, c + 3);
   }
-  int c = Cx;
-  for (; c + 4 < Cx + Ch; c += 4) {
-    chunk(I0{}, F_{}, T_{}, c);
-    chunk(I1{}, F_{}, T_{}, c + 1);
-    chunk(I2{}, F_{}, T_{}, c + 2);
-    chunk(I3{}, F_{}, T_{}, c + 3);
+  chunk(I0{}, T_{}, T_{}, T_{}, c);
+  chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
+  chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
+  chunk(I3{}, T_{}, T_{}, F_{}, c + 3);  // the next chunk is the first h chunk
+  for (c = Cx; c + 4 < Cx + Ch; c += 4) {
+    chunk(I0{}, F_{}, T_{}, F_{}, c);
+    chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
+    chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
+    chunk(I3{}, F_{}, T_{}, F_{}, c + 3);
   }
-  chunk(I0{}, F_{}, T_{}, c);
-  chunk(I1{}, F_{}, T_{}, c + 1);
-  chunk(I2{}, F_{}, T_{}, c + 2);
-  chunk(I3{}, F_{}, F_{}, c + 3);
+  chunk(I0{}, F_{}, T_{}, F_{}, c);
+  chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
+  chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
+  chunk(I3{}, F_{}, F_{}, F_{}, c + 3);
+#ifdef GO2PI_DIAG_CLOCK
+  if (st && wave == 0 && lane == 0) st[44] = __builtin_amdgcn_s_memtime();
+#endif
   float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
@@ -1327,14 +1353,18 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float zg = sigmoid_fast(z[i][e]);
-      const float rg = sigmoid_fast(r[i][e]);
-      const float hv = 2.f * sigmoid_fast(2.f * (nx[i][e] + rg * nh[i][e])) - 1.f;  // tanh, ~1e-7 abs
+      const float zg = sigmoid_fast(z[i][e] + f4c(bz[i], e));
+      const float rg = sigmoid_fast(r[i][e] + f4c(br[i], e));
+      const float nxe = nx[i][e] + f4c(bx[i], e), nhe = nh[i][e] + f4c(bh[i], e);
+      const float hv = 2.f * sigmoid_fast(2.f * (nxe + rg * nhe)) - 1.f;  // tanh, ~1e-7 abs
       o[e] = (1.f - zg) * hv + zg * f4c(ho, e);
     }
     hn[i] = make_float4(o[0], o[1], o[2], o[3]);
     *reinterpret_cast<float4 *>(yrow + i * 16) = hn[i];
   }
+#ifdef GO2PI_DIAG_CLOCK
+  if (st && wave == 0 && lane == 0) st[45] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 // One policy step of the pipeline (the observation tile is being staged into bufA).
@@ -1358,7 +1388,14 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *X0, float *Y
   int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
 #pragma unroll
   for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
+  // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
+  // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
+  // weight stream, whose waits would otherwise cover them); the head's bias to registers
+  if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
+  float4 hbv[1];
+  load_bias<1>(hbv, P.L[nh].bias, wave < HT ? wave : 0, P.L[nh].N_pad >> 4, lane);
   float4 f[4][TPW];
+  asm volatile("" ::: "memory");  // the DMA and bias loads stay ahead of the ring's first loads
   {
     const WStream w0(P.L[0].w);
     const int cs0 = (P.L[0].N_pad >> 4) * 1024;
@@ -1367,17 +1404,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *X0, float *Y
 #pragma unroll
       for (int i = 0; i < TPW; ++i) f[d][i] = w0.ld(vo[i], d * cs0);
   }
-  // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
-  // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
-  // weight stream, whose waits would otherwise cover them); the head's bias to registers
-  if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
-  float4 hbv[1];
-  load_bias<1>(hbv, P.L[nh].bias, wave < HT ? wave : 0, P.L[nh].N_pad >> 4, lane);
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 42] = __builtin_amdgcn_s_memtime();
 #endif
-  lds_dma_wait();   // the observation and bias tiles (this wave's direct-to-LDS loads)
-  __syncthreads();  // layer 0's input rows are complete in X0 (and the biases in LDS)
+  // layer 0's input rows are complete in X0 and the biases in LDS (this wave's
+  // direct-to-LDS loads, older than the ring's); the ring's loads stay in flight
+  wg_barrier_vm<RD * TPW>();
 #ifdef GO2PI_DIAG_CLOCK
   if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1724,12 +1756,11 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       static_assert(NW == 4, "one wave per SIMD");
       float *X0 = bufA, *Y0 = bufB;
       if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
-        lds_dma_wait();
-        __syncthreads();  // x in bufA, the hidden rows in bufH
-        auto carry = [&](auto gt_k) {  // the pipelined cell: h' to bufB, registers, and the carry
+        auto carry = [&](auto gt_k) {  // (w4_gru waits for the x / h staging and barriers itself)  // the pipelined cell: h' to bufB, registers, and the carry
           constexpr int GT = decltype(gt_k)::value;
           float4 hn[GT];
-          w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn);
+          w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
+                     P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr);
           if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's hidden state: once, from registers
             float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
 #pragma unroll
@@ -1745,6 +1776,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         } else if (H == 128) {
           carry(std::integral_constant<int, 2>{});
         } else {
+          lds_dma_wait();
+          __syncthreads();  // x in bufA, the hidden rows in bufH
           gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
           __syncthreads();
           for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {

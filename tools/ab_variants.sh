@@ -29,7 +29,7 @@ export GO2PI_DIAG_STAMPS=1
 for v in ${CLOCKS:-}; do
   for w in ${CLOCK_WAVES:-8}; do
     GO2PI_LIB=$D/libgo2pi_$v.so timeout -k 10 120 python3 $R/tools/clock_probe.py --model ${MODEL:-go2_mlp_512} --waves $w > $O/clock_${v}_w$w.json 2> $O/clock_${v}_w$w.err || { echo "clock $v failed"; tail -5 $O/clock_${v}_w$w.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'], 'sub', d.get('pipeline_layer1_subphases'), 'init', d.get('init_subphases'))"
+    python3 -c "import json;d=json.load(open('$O/clock_${v}_w$w.json'));print('$v waves $w', d['wg_cycles_median'], d['event_us_per_launch'], d['phase_cycles_median']); print('   layer1 marks', d['layer1_wave_marks'], 'sub', d.get('pipeline_layer1_subphases'), 'init', d.get('init_subphases'), 'gru', d.get('gru_stage'))"
   done
 done
 unset GO2PI_DIAG_STAMPS

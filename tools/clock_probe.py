@@ -80,6 +80,11 @@ def main():
         for k, nm in ((40, "descriptors"), (41, "obs_issued"), (42, "barrier_reached")):
             if np.all(st[:, k] > 0):
                 init_sub[nm] = float(np.median(st[:, k] - st[:, 0]))
+    gru_sub = {}
+    if np.all(st[:, 43] > 0):  # pipelined GRU stage (wave 0): entry, contraction done, epilogue done
+        gru_sub = {"entry": float(np.median(st[:, 43] - st[:, 0])),
+                   "contraction": float(np.median(st[:, 44] - st[:, 43])),
+                   "epilogue": float(np.median(st[:, 45] - st[:, 44]))}
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
         names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
@@ -100,7 +105,7 @@ def main():
            "wg_end_spread_us": float((st[:, 3].max() - st[:, 3].min()) / 100),
            "phase_cycles_median": phases,
            "layer1_wave_marks": waves_l1,  # [entry, contraction done, epilogue done, barrier] cycles
-           "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub}
+           "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub, "gru_stage": gru_sub}
     print(json.dumps(out))
 
 
