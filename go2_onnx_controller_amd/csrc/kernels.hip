@@ -1518,6 +1518,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, float *X0, float *Y
       for (int i = 0; i < TPW; ++i) v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
 #pragma unroll
       for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
+#ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
+      if (sub) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 46 + wave] = __builtin_amdgcn_s_memtime();
+#endif
       if constexpr (HO) {
         publish();
         [&]<int... I>(std::integer_sequence<int, I...>) {

@@ -75,6 +75,8 @@ def main():
         a, b, c, z = st[:, 28 + 3 * w], st[:, 29 + 3 * w], st[:, 30 + 3 * w], st[:, 16 + 3 * w]
         if np.all(a > 0) and np.all(z > 0):
             sub_l1[w] = [float(np.median(a - z)), float(np.median(b - z)), float(np.median(c - z))]
+            if np.all(st[:, 46 + w] > 0):  # epilogue issued (slot 46 + w), first in the list
+                sub_l1[w].insert(0, float(np.median(st[:, 46 + w] - z)))
     init_sub = {}
     if np.all(st[:, 40] > 0):  # init sub-phases (slots 40-42) relative to the workgroup start
         for k, nm in ((40, "descriptors"), (41, "obs_issued"), (42, "barrier_reached")):
