@@ -204,7 +204,8 @@ def load_pmc(workload, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--settle-s", type=float, default=0.3, help="untimed clock-settle phase before the warmup")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="go2_mlp_512_b4096", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="override robots per GPU")
@@ -248,6 +249,14 @@ def main():
     stream = torch.cuda.Stream(dev)  # the stream every timed launch goes to
 
     launch = eng.device_launcher(obs.data_ptr(), act.data_ptr(), batch, stream.cuda_stream)
+    # clock settle (untimed): an idle MI355X needs tens of ms of load before its
+    # clocks reach steady state; without this a short default run times the ramp
+    # (200 launches: 42.0 us each straight from idle vs 38.8 us settled)
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle_s:
+        for _ in range(50):
+            launch()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize(dev)
