@@ -7,6 +7,7 @@
 // Errors throw std::runtime_error (the reference lets Ort::Exception escape).
 #include "../../include/onnx_actor.hpp"
 
+#include <cstdlib>
 #include <iostream>
 #include <stdexcept>
 
@@ -53,6 +54,11 @@ ONNXActor::ONNXActor(const std::string &model_path, const std::span<float> obser
   go2pi_default_opts(&opts);
   opts.log_level = static_cast<int32_t>(log_level);
   opts.max_batch = 64;  // one robot per act(); keep device buffers small
+  // act() is one robot's tick at the controller's 50 Hz (controller.cpp:61): a
+  // resident kernel serves it without a launch per call and leaves after 100 ms
+  // without one (GO2PI_RESIDENT_MS overrides; 0 = one launch per call).
+  opts.resident_ms = 100;
+  if (const char *v = std::getenv("GO2PI_RESIDENT_MS")) opts.resident_ms = std::atoi(v);
   check(go2pi_create(model_path.c_str(), &opts, &impl_->engine), "cannot load model");
   impl_->input_name = name_of(impl_->engine, 0);
   impl_->output_name = name_of(impl_->engine, 1);

@@ -125,4 +125,19 @@ int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int wa
 int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, int batch, unsigned epoch0,
                        unsigned long long *gran, int gstride, unsigned *err, unsigned *done, void *stream);
 
+// Resident batch <= GO2PI_SMALL_MAXB path (resident.hip): ONE launch serves act()
+// requests until it is told to leave or sits idle for idle_ticks of the 100 MHz
+// wall clock. req: host-mapped [1 + SMALL_MAXB * in_dim] {tag, value} granules,
+// req[0] = {epoch, batch} (tag GO2PI_RES_LEAVE: leave), req[1 + i] = {epoch, obs[i]};
+// act: host-mapped [SMALL_MAXB][out_dim]; done: set to the epoch once the action is
+// written, to GO2PI_RES_LEAVE when the kernel leaves. Layer-l granules carry tag
+// epoch + 1 + l. gran must be zeroed before every launch (a leaving workgroup tags
+// its slots GO2PI_RES_LEAVE so waiting consumers leave too). mirror: device
+// [1 + SMALL_MAXB * in_dim] granules, workgroup 0's copy of each request for the
+// other workgroups (zeroed before every launch, like gran).
+#define GO2PI_RES_LEAVE 0xFFFFFFFFu
+int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
+                    unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
+                    unsigned *done, unsigned long long idle_ticks, void *stream);
+
 }  // namespace go2pi

@@ -1,0 +1,332 @@
+// policy_resident_kernel — the batch-1 act() path without a launch per call
+// (north_star: "a persistent-kernel / hipGraph path captures one control step
+// to kill launch latency at batch=1").
+//
+// The reference runs one onnxruntime Session::Run per control tick
+// (onnx_inference/src/cpp/onnx_actor.cpp:38-48, called from
+// onnx_controller/src/controller.cpp:215 every 20 ms). policy_latency_kernel
+// (kernels.hip) does that tick in one launch; this kernel stays resident
+// between ticks instead, so a tick costs no launch and no dispatch:
+//
+//  * the host writes the observation as 8-byte {epoch, value} granules into
+//    pinned host-mapped memory, then a header granule {epoch, batch};
+//  * wave 0 of workgroup 0 polls the header together with the first
+//    observation granules in one system-scope sweep (the data IS the flag,
+//    cdna_hip_programming.md Guideline 16 recipe R2), so the observation has
+//    arrived when the request is seen, and mirrors the request into device
+//    memory for the other workgroups (with every workgroup polling the host,
+//    the 32 pollers of the 48->512^3->12 policy made a call 4.6 us SLOWER than
+//    a launch per call; the shipped policy's 8 were 5 us faster);
+//  * the layers then run exactly as in policy_latency_kernel (same per-output
+//    summation order: the two paths are bit-identical), with layer-l granules
+//    tagged epoch + 1 + l; workgroup 0 writes the action rows to host-mapped
+//    memory and sets the host-mapped done word to the epoch.
+//
+// Leaving: on a GO2PI_RES_LEAVE header, on idle_ticks of the 100 MHz wall clock
+// without a request, or when a sweep meets a GO2PI_RES_LEAVE-tagged granule, a
+// workgroup tags every granule slot it produces GO2PI_RES_LEAVE (so consumers
+// still waiting on it leave at once instead of spinning to their bound) and
+// exits; workgroup 0 sets done = GO2PI_RES_LEAVE. Every spin is bounded, so the
+// grid always drains. The host relaunches on its next request.
+#include <hip/hip_runtime.h>
+
+#include "device_fn.hpp"
+#include "program.hpp"
+
+namespace go2pi {
+
+namespace {
+
+constexpr int RES_WAVES = 8;
+constexpr int RES_MAXS = 8;  // chunk slots per wave held in registers (K_pad <= 1024)
+constexpr int RES_POLL = 2;  // header + observation granules per lane in the idle poll (<= 127 obs floats)
+
+typedef unsigned long long u64;
+
+// One wave sweeps n granules until every tag equals `tag`: 1 done, -1 a producer
+// left (GO2PI_RES_LEAVE tag), 0 timeout (err set).
+template <int SCOPE>
+__device__ __forceinline__ int sweep(const u64 *g, int n, unsigned tag, float *dst, unsigned *err, int lane) {
+  constexpr int U = 8;
+  u64 *gm = const_cast<u64 *>(g);
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true, leave = false;
+    for (int base = 0; base < n; base += 64 * U) {
+      u64 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __hip_atomic_load(gm + min(base + u * 64 + lane, n - 1), __ATOMIC_RELAXED, SCOPE);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * 64 + lane;
+        if (i < n) {
+          const unsigned t = (unsigned)(v[u] >> 32);
+          ok &= t == tag;
+          leave |= t == GO2PI_RES_LEAVE;
+          dst[i] = __uint_as_float((unsigned)v[u]);
+        }
+      }
+    }
+    if (__any(leave)) return -1;
+    if (__all(ok)) return 1;
+    if (spins > (1u << 22)) {
+      if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Wave-level wait for the next request in `q` ([0] = {epoch, batch} header,
+// [1 + i] = {epoch, obs[i]}): the header and the first observation granules are
+// read in one sweep, so for a small request the observation has arrived when the
+// request is seen. Leaves (leave = 1) on a GO2PI_RES_LEAVE header or idle_ticks
+// of the 100 MHz wall clock without a request.
+template <int SCOPE>
+__device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned last, u64 idle_ticks, float *obsv,
+                                             unsigned *err, int lane, int &leave, unsigned &e, int &B) {
+  u64 *qm = const_cast<u64 *>(q);
+  const u64 t0 = wall_clock64();
+  const int npoll = min(1 + in_dim, 64 * RES_POLL);
+  leave = 0;
+  for (;;) {
+    u64 v[RES_POLL];
+#pragma unroll
+    for (int u = 0; u < RES_POLL; ++u)
+      if (u * 64 < npoll) v[u] = __hip_atomic_load(qm + min(u * 64 + lane, npoll - 1), __ATOMIC_RELAXED, SCOPE);
+    const u64 h = __shfl(v[0], 0);
+    const unsigned tag = (unsigned)(h >> 32);
+    if (tag == GO2PI_RES_LEAVE) {
+      leave = 1;
+      return;
+    }
+    if (tag != 0u && tag != last) {
+      e = tag;
+      B = min(max((int)(unsigned)h, 1), GO2PI_SMALL_MAXB);
+      const int n = B * in_dim;  // observation granules q[1 .. n]
+      if (1 + n <= npoll) {
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < RES_POLL; ++u) {
+          const int i = u * 64 + lane;
+          if (u * 64 < npoll && i >= 1 && i <= n) {
+            ok &= (unsigned)(v[u] >> 32) == e;
+            obsv[i - 1] = __uint_as_float((unsigned)v[u]);
+          }
+        }
+        if (__all(ok)) return;
+      } else {
+        if (sweep<SCOPE>(q + 1, n, e, obsv, err, lane) != 1) leave = 1;
+        return;
+      }
+    }
+    if (wall_clock64() - t0 > idle_ticks) {
+      leave = 1;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Tag every granule this workgroup produces GO2PI_RES_LEAVE (all layers, all rows).
+__device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, int tid) {
+  for (int l = 0; l + 1 < P.nl; ++l) {
+    const DevLayer &L = P.L[l];
+    if (g >= (L.N_pad >> 4)) continue;
+    if (tid < GO2PI_SMALL_MAXB * 16) {
+      const int b = tid >> 4, n = g * 16 + (tid & 15);
+      __hip_atomic_store(gran + (size_t)l * gstride + b * L.N_pad + n, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
+                                                                         const u64 *req, float *act, u64 *gran,
+                                                                         int gstride, u64 *mirror, unsigned *err,
+                                                                         unsigned *done, u64 idle_ticks) {
+  const DevProgram &P = *Pd;
+  extern __shared__ float4 lds4[];
+  float *xs = reinterpret_cast<float *>(lds4);                       // [B][K_pad] layer input
+  float *part = xs + GO2PI_SMALL_MAXB * P.lds_stride;                // [waves][B][16] partial sums
+  int *st = reinterpret_cast<int *>(part + RES_WAVES * GO2PI_SMALL_MAXB * 16);  // [0] leave, [1] epoch, [2] batch
+  float *obsv = reinterpret_cast<float *>(st + 4);                   // [B][in_dim] the request's observation
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int in_dim = P.in_dim;
+  unsigned last = 0;
+  // The weight fragments of the next layer this workgroup owns a tile of are
+  // loaded one layer ahead, and those of its first layer before each request
+  // wait, so a request meets them in registers (the launch-per-call kernel
+  // fetches layer 0's from L2 after its launch).
+  auto owned_from = [&](int l) {
+    while (l < P.nl && g >= (P.L[l].N_pad >> 4)) ++l;
+    return l;  // P.nl: none
+  };
+  float4 wr[RES_MAXS];
+  float bv = 0.f;
+  auto load_layer = [&](int l) {
+    const DevLayer &L = P.L[l];
+    const int T = L.N_pad >> 4, C = L.K_pad >> 4;
+    const float4 *W = reinterpret_cast<const float4 *>(L.w) + (size_t)g * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < RES_MAXS; ++s) {
+      const int c = wave + s * RES_WAVES;
+      wr[s] = c < C ? W[(size_t)c * T * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
+  };
+  const int l_first = owned_from(0);
+  load_layer(l_first);
+
+  for (;;) {
+    // ---- wait for a request. Workgroup 0 polls the host (header + the first
+    // observation granules in one sweep) and mirrors the request into device
+    // memory; the others poll that mirror, so one wave, not the grid, reads
+    // host memory over PCIe while idle.
+    if (wave == 0) {
+      int leave = 0, B = 0;
+      unsigned e = 0;
+      if (g == 0) {
+        wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B);
+        const int n = leave ? 0 : B * in_dim;
+        for (int i = lane; i < n; i += 64)
+          __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+          __hip_atomic_store(mirror, leave ? ((u64)GO2PI_RES_LEAVE << 32) : (((u64)e << 32) | (unsigned)B),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        wait_request<__HIP_MEMORY_SCOPE_AGENT>(mirror, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B);
+      }
+      if (lane == 0) {
+        st[0] = leave;
+        st[1] = (int)e;
+        st[2] = B;
+      }
+    }
+    __syncthreads();
+    if (st[0]) break;
+    const unsigned e = (unsigned)st[1];
+    const int B = st[2];
+    last = e;
+    bool left = false;
+
+    // ---- the layers (policy_latency_kernel's body; tags e + 1 + l)
+    for (int l = 0; l < P.nl; ++l) {
+      const DevLayer &L = P.L[l];
+      const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
+      if (g >= T) continue;  // this workgroup owns no tile of layer l
+      // wr / bv hold layer l (prefetched)
+      if (l == 0) {
+        for (int i = tid; i < B * K_pad; i += RES_WAVES * 64) {
+          const int b = i / K_pad, k = i - b * K_pad;
+          xs[i] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
+        }
+      } else if (wave == 0) {
+        if (sweep<__HIP_MEMORY_SCOPE_AGENT>(gran + (size_t)(l - 1) * gstride, B * K_pad, e + (unsigned)l, xs, err,
+                                            lane) != 1 &&
+            lane == 0)
+          st[0] = 1;
+      }
+      __syncthreads();
+      if (st[0]) {
+        left = true;
+        break;
+      }
+      float p[GO2PI_SMALL_MAXB];
+#pragma unroll
+      for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
+      const int koff = (lane >> 4) << 2;
+#pragma unroll
+      for (int s = 0; s < RES_MAXS; ++s) {
+        const int c = wave + s * RES_WAVES;
+        if (c >= C) break;
+#pragma unroll
+        for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+          if (b < B) {
+            const float4 a = *reinterpret_cast<const float4 *>(xs + b * K_pad + c * 16 + koff);
+            p[b] = fmaf(a.x, wr[s].x, p[b]);
+            p[b] = fmaf(a.y, wr[s].y, p[b]);
+            p[b] = fmaf(a.z, wr[s].z, p[b]);
+            p[b] = fmaf(a.w, wr[s].w, p[b]);
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+        p[b] += __shfl_xor(p[b], 16);
+        p[b] += __shfl_xor(p[b], 32);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int b = 0; b < GO2PI_SMALL_MAXB; ++b)
+          if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
+      }
+      const float bcur = bv;
+      {
+        const int ln = owned_from(l + 1);  // the next owned layer, else the first of the next request
+        load_layer(ln < P.nl ? ln : l_first);
+      }
+      __syncthreads();
+      if (wave == 0 && lane < 16) {
+        const int n = g * 16 + lane;
+        const bool lastl = l == P.nl - 1;
+        for (int b = 0; b < B; ++b) {
+          float s = 0.f;
+          for (int w2 = 0; w2 < RES_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
+          const float v = act_fn(L.act, L.alpha, s + bcur);
+          if (lastl) {
+            if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
+            if (b == B - 1 && g == 0) {
+              // every action store of this tile drained and system-visible before the done word
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              if (lane == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          } else {
+            const u64 gv = ((u64)(e + 1u + (unsigned)l) << 32) | __float_as_uint(v);
+            __hip_atomic_store(gran + (size_t)l * gstride + b * L.N_pad + n, gv, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      __syncthreads();  // xs / part reused by the next layer
+    }
+    if (left) break;
+  }
+  // ---- leave: consumers still waiting on this workgroup's slots leave too
+  tag_leave(P, gran, gstride, g, tid);
+  if (g == 0 && tid == 0)
+    __hip_atomic_store(mirror, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (g == 0 && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
+                    unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
+                    unsigned *done, unsigned long long idle_ticks, void *stream) {
+  if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
+  int grid = 1;
+  for (int l = 0; l < p.nl; ++l) {
+    if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
+    grid = std::max(grid, p.L[l].N_pad >> 4);
+  }
+  const size_t lds = sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 +
+                                      4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(policy_resident_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (a != hipSuccess) return (int)a;
+  }
+  hipLaunchKernelGGL(policy_resident_kernel, dim3(grid), dim3(RES_WAVES * 64), lds,
+                     reinterpret_cast<hipStream_t>(stream), p_dev, req, act, gran, gstride, mirror, err, done,
+                     idle_ticks);
+  return (int)hipGetLastError();
+}
+
+}  // namespace go2pi

@@ -57,6 +57,7 @@ class Opts(ctypes.Structure):
         ("action_tanh", ctypes.c_int32),
         ("action_clip", ctypes.c_float),
         ("action_scale", ctypes.c_float),
+        ("resident_ms", ctypes.c_int32),
     ]
 
 
@@ -158,7 +159,7 @@ class Engine:
 
     def __init__(self, model, device=0, max_batch=4096, use_graph=True, waves=0, small_batch=0,
                  obs_mean=None, obs_std=None, obs_clip=0.0, action_tanh=False, action_clip=0.0,
-                 action_scale=0.0, log_level=2):
+                 action_scale=0.0, log_level=2, resident_ms=0):
         L = lib()
         o = Opts()
         L.go2pi_default_opts(ctypes.byref(o))
@@ -175,6 +176,7 @@ class Engine:
             o.obs_std = s.ctypes.data
         o.obs_clip, o.action_tanh = float(obs_clip), int(bool(action_tanh))
         o.action_clip, o.action_scale = float(action_clip), float(action_scale)
+        o.resident_ms = int(resident_ms)  # > 0: batch <= 8 run() served by a resident kernel
         h = ctypes.c_void_p()
         if isinstance(model, (bytes, bytearray)):
             buf = bytes(model)

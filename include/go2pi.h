@@ -62,6 +62,12 @@ typedef struct go2pi_opts {
   float action_clip;     /* > 0: clamp action to [-action_clip, action_clip]
                             (the caller's kActionLimit clamp, controller.cpp:217-223) */
   float action_scale;    /* != 0 and != 1: action <- action * action_scale (after clip) */
+  /* > 0: go2pi_run at batch <= 8 is served by a RESIDENT kernel (no launch per call:
+     the request and the observation travel as tagged granules in host-mapped memory);
+     the kernel leaves after this many ms without a request and is relaunched by the
+     next call. 0 (default): one launch per call. Any other call on the engine first
+     stops the resident kernel. */
+  int32_t resident_ms;
 } go2pi_opts;
 
 void go2pi_default_opts(go2pi_opts *opts);

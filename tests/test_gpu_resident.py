@@ -1,0 +1,112 @@
+"""GPU: the resident batch <= 8 act() path (opts.resident_ms > 0, resident.hip).
+
+One launch serves every go2pi_run at batch <= 8: the observation and the
+request header travel as {epoch, value} granules in host-mapped memory. The
+layers are policy_latency_kernel's, so the resident path must be BIT-identical
+to the one-launch-per-call path (and within the 1e-5 contract of the fp64
+oracle). Also covered: the kernel leaving on idle (a request racing that exit is
+served by a relaunch), another engine call in between (the kernel is stopped
+and relaunched), and destroy while resident.
+"""
+import time
+
+import numpy as np
+import pytest
+
+from conftest import SHIPPED, abs_err, realistic_obs
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _models(synth_path):
+    return {"shipped": SHIPPED, "mlp512": synth_path("go2_mlp_512")}
+
+
+@pytest.mark.parametrize("name", ["shipped", "mlp512"])
+def test_resident_bitwise_vs_launch_per_call(synth_path, name):
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    path = _models(synth_path)[name]
+    ref = mlp_ref.MlpRef.from_onnx(path)
+    with Engine(path, max_batch=64, resident_ms=500) as r, Engine(path, max_batch=64) as p:
+        rng = np.random.default_rng(7)
+        for i, B in enumerate([1, 1, 2, 3, 1, 8, 5, 1, 4, 1] * 3):
+            x = (realistic_obs(B, seed=i) if name == "shipped"
+                 else rng.standard_normal((B, r.in_dim)).astype(np.float32))
+            y = r.run(x)
+            assert y.shape == (B, r.out_dim)
+            assert np.array_equal(y, p.run(x)), f"call {i} B={B}: resident != launch-per-call"
+            assert abs_err(y, ref.f64(x)) <= TOL
+
+
+def test_resident_known_answers():
+    """The reference drivers' inputs (src/cpp/main.cpp:32 zeros, src/python/main.py:20 twos)."""
+    import os
+    from conftest import GOLDEN, rel_err
+    from go2_onnx_controller_amd import Engine
+    g = np.load(os.path.join(GOLDEN, "golden_shipped.npz"))
+    with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
+        for _ in range(3):
+            for name in ("zeros", "twos"):
+                assert rel_err(e.run(g[f"{name}_x"]), g[f"{name}_y"]) <= TOL, name
+
+
+def test_resident_interleaved_with_batched_calls(synth_path):
+    """A batched call parks the resident kernel; the next small call relaunches it."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    path = synth_path("go2_mlp_512")
+    ref = mlp_ref.MlpRef.from_onnx(path)
+    rng = np.random.default_rng(3)
+    with Engine(path, max_batch=4096, resident_ms=500) as e:
+        for i in range(4):
+            x1 = rng.standard_normal((1, 48)).astype(np.float32)
+            assert abs_err(e.run(x1), ref.f64(x1)) <= TOL
+            xb = rng.standard_normal((256 * (i + 1), 48)).astype(np.float32)
+            assert abs_err(e.run(xb), ref.f64(xb)) <= TOL
+            e.sync()
+            x2 = rng.standard_normal((3, 48)).astype(np.float32)
+            assert abs_err(e.run(x2), ref.f64(x2)) <= TOL
+
+
+def test_resident_idle_exit_and_relaunch():
+    """resident_ms = 4: requests after 0-12 ms pauses meet a live kernel, one near its
+    idle deadline (the host relaunches past half of it) or one that has left."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    ref = mlp_ref.MlpRef.from_onnx(SHIPPED)
+    rng = np.random.default_rng(11)
+    with Engine(SHIPPED, max_batch=8, resident_ms=4) as e:
+        for i in range(60):
+            x = realistic_obs(1 + i % 3, seed=100 + i)
+            assert abs_err(e.run(x), ref.f64(x)) <= TOL, f"call {i}"
+            time.sleep(float(rng.uniform(0.0, 0.012)))
+
+
+def test_resident_destroy_while_live(synth_path):
+    from go2_onnx_controller_amd import Engine
+    path = synth_path("go2_mlp_512")
+    x = np.ones((1, 48), np.float32)
+    for _ in range(5):
+        e = Engine(path, max_batch=8, resident_ms=10000)
+        e.run(x)
+        t0 = time.perf_counter()
+        e.close()  # the kernel leaves on the LEAVE header, not on its 10 s idle bound
+        assert time.perf_counter() - t0 < 1.0
+
+
+def test_resident_two_engines(synth_path):
+    """Two resident kernels on one device, served alternately."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    pa, pb = SHIPPED, synth_path("go2_mlp_512")
+    ra, rb = mlp_ref.MlpRef.from_onnx(pa), mlp_ref.MlpRef.from_onnx(pb)
+    rng = np.random.default_rng(5)
+    with Engine(pa, max_batch=8, resident_ms=500) as a, Engine(pb, max_batch=8, resident_ms=500) as b:
+        for i in range(20):
+            xa = realistic_obs(1, seed=i)
+            xb = rng.standard_normal((2, 48)).astype(np.float32)
+            assert abs_err(a.run(xa), ra.f64(xa)) <= TOL
+            assert abs_err(b.run(xb), rb.f64(xb)) <= TOL

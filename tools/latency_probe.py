@@ -16,12 +16,14 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--small-batch", type=int, default=0)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--resident-ms", type=int, default=0)
     args = ap.parse_args()
     import numpy as np
     from go2_onnx_controller_amd import Engine, synth
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
                         "model.onnx") if args.model == "shipped" else synth.ensure_model(args.model)
-    with Engine(path, max_batch=64, use_graph=not args.no_graph, small_batch=args.small_batch) as e:
+    with Engine(path, max_batch=64, use_graph=not args.no_graph, small_batch=args.small_batch,
+                resident_ms=args.resident_ms) as e:
         x = np.random.default_rng(2).standard_normal((args.batch, e.in_dim)).astype(np.float32)
         y = np.empty((args.batch, e.out_dim), np.float32)
         for _ in range(300):
@@ -34,7 +36,7 @@ def main():
             ts.append((time.perf_counter_ns() - t0) / 1e3)
     ts.sort()
     print(f"{args.model} B={args.batch} graph={not args.no_graph} small={args.small_batch}: "
-          f"p50 {ts[len(ts)//2]:.2f} us  p99 {ts[int(len(ts)*0.99)]:.2f} us  min {ts[0]:.2f} us")
+          f"resident={args.resident_ms}: p50 {ts[len(ts)//2]:.2f} us  p99 {ts[int(len(ts)*0.99)]:.2f} us  min {ts[0]:.2f} us")
 
 
 if __name__ == "__main__":
