@@ -2028,8 +2028,12 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
         const int b = e / K_pad, k = e - b * K_pad;
         xs[e] = k < P.in_dim ? prologue(P, src[(size_t)b * P.in_dim + k], k) : 0.f;
       }
-    } else if (wave == 0) {
-      if (!sweep_layer(gran + (size_t)(l - 1) * gstride, B * K_pad, epoch0 + (unsigned)(l - 1), xs, err, lane))
+    } else {
+      // every wave sweeps its own 512 granules (8 per lane, all in flight), not
+      // wave 0 alone in B * K_pad / 512 serial rounds
+      const int n = B * K_pad, lo = wave * 512;
+      if (lo < n && !sweep_layer(gran + (size_t)(l - 1) * gstride + lo, min(512, n - lo), epoch0 + (unsigned)(l - 1),
+                                 xs + lo, err, lane))
         abort_flag = 1;
     }
     __syncthreads();

@@ -224,9 +224,13 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           const int b = i / K_pad, k = i - b * K_pad;
           xs[i] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
         }
-      } else if (wave == 0) {
-        if (sweep<__HIP_MEMORY_SCOPE_AGENT>(gran + (size_t)(l - 1) * gstride, B * K_pad, e + (unsigned)l, xs, err,
-                                            lane) != 1 &&
+      } else {
+        // every wave sweeps its own 512 granules (8 per lane, all in flight): at
+        // batch 8 one wave's eight serial rounds cost ~20 us per call
+        const int n = B * K_pad, lo = wave * 512;
+        if (lo < n &&
+            sweep<__HIP_MEMORY_SCOPE_AGENT>(gran + (size_t)(l - 1) * gstride + lo, min(512, n - lo), e + (unsigned)l,
+                                            xs + lo, err, lane) != 1 &&
             lane == 0)
           st[0] = 1;
       }
