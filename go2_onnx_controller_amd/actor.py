@@ -14,6 +14,7 @@ Both run on the GPU through libgo2pi.so; there is no CPU fallback.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -36,6 +37,9 @@ class ONNXActor:
         self._obs = observation
         self._act = action
         engine_kwargs.setdefault("max_batch", 64)
+        # as the C++ shim: a resident kernel serves act() (no launch per tick), leaving
+        # after 100 ms without one; GO2PI_RESIDENT_MS=0 -> one launch per call
+        engine_kwargs.setdefault("resident_ms", int(os.environ.get("GO2PI_RESIDENT_MS", "100")))
         self._engine = Engine(model_path, log_level=log_level, **engine_kwargs)
         self.model_path = model_path
         self.input_name, self.input_shape = self._engine.inputs[0]

@@ -17,10 +17,12 @@
 //    memory for the other workgroups (with every workgroup polling the host,
 //    the 32 pollers of the 48->512^3->12 policy made a call 4.6 us SLOWER than
 //    a launch per call; the shipped policy's 8 were 5 us faster);
-//  * the layers then run exactly as in policy_latency_kernel (same per-output
-//    summation order: the two paths are bit-identical), with layer-l granules
-//    tagged epoch + 1 + l; workgroup 0 writes the action rows to host-mapped
-//    memory and sets the host-mapped done word to the epoch.
+//  * every workgroup computes all of layer 0 itself (local_layer0: no hand-off
+//    for its outputs); layers 1.. run as in policy_latency_kernel (same
+//    per-output summation order), with layer-l granules tagged epoch + 1 + l;
+//    workgroup 0 writes the action rows to host-mapped memory and sets the
+//    host-mapped done word to the epoch. (GO2PI_RES_TILED0=1: layer 0 tiled
+//    too, bit-identical to the launch-per-call path.)
 //
 // Leaving: on a GO2PI_RES_LEAVE header, on idle_ticks of the 100 MHz wall clock
 // without a request, or when a sweep meets a GO2PI_RES_LEAVE-tagged granule, a
@@ -29,6 +31,8 @@
 // exits; workgroup 0 sets done = GO2PI_RES_LEAVE. Every spin is bounded, so the
 // grid always drains. The host relaunches on its next request.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "device_fn.hpp"
 #include "program.hpp"
@@ -128,8 +132,8 @@ __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned 
 }
 
 // Tag every granule this workgroup produces GO2PI_RES_LEAVE (all layers, all rows).
-__device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, int tid) {
-  for (int l = 0; l + 1 < P.nl; ++l) {
+__device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, int tid, int l0) {
+  for (int l = l0; l + 1 < P.nl; ++l) {
     const DevLayer &L = P.L[l];
     if (g >= (L.N_pad >> 4)) continue;
     if (tid < GO2PI_SMALL_MAXB * 16) {
@@ -140,18 +144,72 @@ __device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, in
   }
 }
 
+// Layer 0 computed by EVERY workgroup for itself ("local layer 0"), so its
+// outputs need no hand-off: thread tid owns output n = tid % N0 over k-chunk
+// slice ks = tid / N0 (KS = 512 / N0 slices), its NF fragments held in registers
+// for the kernel's life; the input rows come from LDS as broadcast float4 reads.
+// One fma chain per output in k order (KS partials summed in slice order), so
+// this path is deterministic but not bit-identical to the launch-per-call one.
+template <int NF>
+__device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (&w0)[NF], float b0, const float *obsv,
+                                             float *x0, float *p0, float *xs, int B, int tid) {
+  const DevLayer &L = P.L[0];
+  const int N0 = L.N_pad, K0 = L.K_pad, KS = (RES_WAVES * 64) / N0;
+  for (int i = tid; i < B * K0; i += RES_WAVES * 64) {
+    const int b = i / K0, k = i - b * K0;
+    x0[i] = k < P.in_dim ? prologue(P, obsv[b * P.in_dim + k], k) : 0.f;
+  }
+  __syncthreads();
+  const int n = tid % N0, ks = tid / N0;
+  const int K1 = P.L[1].K_pad;  // layer 1's input row stride (= N0)
+  for (int b = 0; b < B; ++b) {
+    float acc = 0.f;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      // fragment f: chunk c = ks + KS * (f >> 2), quad q = f & 3 -> k = 16c + 4q .. +3
+      const int k = 16 * (ks + KS * (f >> 2)) + 4 * (f & 3);
+      const float4 a = *reinterpret_cast<const float4 *>(x0 + b * K0 + k);
+      acc = fmaf(a.x, w0[f].x, acc);
+      acc = fmaf(a.y, w0[f].y, acc);
+      acc = fmaf(a.z, w0[f].z, acc);
+      acc = fmaf(a.w, w0[f].w, acc);
+    }
+    if (KS == 1) {
+      xs[b * K1 + n] = act_fn(L.act, L.alpha, acc + b0);
+    } else {
+      p0[(ks * GO2PI_SMALL_MAXB + b) * N0 + n] = acc;
+    }
+  }
+  if (KS > 1) {
+    __syncthreads();
+    for (int i = tid; i < B * N0; i += RES_WAVES * 64) {
+      const int b = i / N0, nn = i - b * N0;
+      float acc = 0.f;
+      for (int s2 = 0; s2 < KS; ++s2) acc += p0[(s2 * GO2PI_SMALL_MAXB + b) * N0 + nn];
+      xs[b * K1 + nn] = act_fn(L.act, L.alpha, acc + L.bias[nn]);
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace
 
+// NF > 0: local layer 0 (above) with NF fragments per thread; 0: layer 0 tiled
+// over the workgroups like every other layer (policy_latency_kernel's order).
+template <int NF>
 __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
                                                                          const u64 *req, float *act, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
                                                                          unsigned *done, u64 idle_ticks) {
+  constexpr bool LOCAL0 = NF > 0;
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
   float *xs = reinterpret_cast<float *>(lds4);                       // [B][K_pad] layer input
   float *part = xs + GO2PI_SMALL_MAXB * P.lds_stride;                // [waves][B][16] partial sums
   int *st = reinterpret_cast<int *>(part + RES_WAVES * GO2PI_SMALL_MAXB * 16);  // [0] leave, [1] epoch, [2] batch
   float *obsv = reinterpret_cast<float *>(st + 4);                   // [B][in_dim] the request's observation
+  float *x0 = obsv + GO2PI_SMALL_MAXB * P.in_dim;                    // LOCAL0: [B][K0] prologued layer-0 input
+  float *p0 = x0 + GO2PI_SMALL_MAXB * P.L[0].K_pad;                  // LOCAL0, KS > 1: [KS][B][N0] partials
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
@@ -161,6 +219,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   // wait, so a request meets them in registers (the launch-per-call kernel
   // fetches layer 0's from L2 after its launch).
   auto owned_from = [&](int l) {
+    if (LOCAL0 && l == 0) l = 1;  // layer 0 has its own registers (w0)
     while (l < P.nl && g >= (P.L[l].N_pad >> 4)) ++l;
     return l;  // P.nl: none
   };
@@ -178,7 +237,20 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
   };
   const int l_first = owned_from(0);
-  load_layer(l_first);
+  if (l_first < P.nl) load_layer(l_first);
+  float4 w0[LOCAL0 ? NF : 1];
+  float b0 = 0.f;
+  if constexpr (LOCAL0) {
+    const DevLayer &L = P.L[0];
+    const int N0 = L.N_pad, KS = (RES_WAVES * 64) / N0, n = tid % N0, ks = tid / N0;
+    const float4 *W = reinterpret_cast<const float4 *>(L.w);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int c = ks + KS * (f >> 2), q = f & 3;
+      w0[f] = W[((size_t)c * (N0 >> 4) + (n >> 4)) * 64 + (n & 15) + 16 * q];
+    }
+    b0 = L.bias[n];
+  }
 
   for (;;) {
     // ---- wait for a request. Workgroup 0 polls the host (header + the first
@@ -214,7 +286,8 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     bool left = false;
 
     // ---- the layers (policy_latency_kernel's body; tags e + 1 + l)
-    for (int l = 0; l < P.nl; ++l) {
+    if constexpr (LOCAL0) local_layer0<NF>(P, w0, b0, obsv, x0, p0, xs, B, tid);
+    for (int l = LOCAL0 ? 1 : 0; l < P.nl; ++l) {
       const DevLayer &L = P.L[l];
       const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
       if (g >= T) continue;  // this workgroup owns no tile of layer l
@@ -224,7 +297,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           const int b = i / K_pad, k = i - b * K_pad;
           xs[i] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
         }
-      } else {
+      } else if (!(LOCAL0 && l == 1)) {  // (local layer 0 left layer 1's input in xs)
         // every wave sweeps its own 512 granules (8 per lane, all in flight): at
         // batch 8 one wave's eight serial rounds cost ~20 us per call
         const int n = B * K_pad, lo = wave * 512;
@@ -301,7 +374,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     if (left) break;
   }
   // ---- leave: consumers still waiting on this workgroup's slots leave too
-  tag_leave(P, gran, gstride, g, tid);
+  tag_leave(P, gran, gstride, g, tid, LOCAL0 ? 1 : 0);
   if (g == 0 && tid == 0)
     __hip_atomic_store(mirror, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (g == 0 && tid == 0) {
@@ -319,18 +392,28 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
     grid = std::max(grid, p.L[l].N_pad >> 4);
   }
+  // local layer 0 where each thread's share of it fits NF = 8 or 16 registers' fragments
+  const int N0 = p.L[0].N_pad, C0 = p.L[0].K_pad >> 4;
+  const int KS = (N0 > 0 && (RES_WAVES * 64) % N0 == 0) ? (RES_WAVES * 64) / N0 : 0;
+  const int nf = (KS > 0 && C0 % KS == 0) ? 4 * (C0 / KS) : 0;
+  const bool local0 = p.nl >= 2 && (nf == 8 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
   const size_t lds = sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 +
-                                      4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim);
+                                      4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim +
+                                      (local0 ? (size_t)GO2PI_SMALL_MAXB * (p.L[0].K_pad + (KS > 1 ? KS * N0 : 0)) : 0));
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  if (lds > 64 * 1024) {
-    const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(policy_resident_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (a != hipSuccess) return (int)a;
-  }
-  hipLaunchKernelGGL(policy_resident_kernel, dim3(grid), dim3(RES_WAVES * 64), lds,
-                     reinterpret_cast<hipStream_t>(stream), p_dev, req, act, gran, gstride, mirror, err, done,
-                     idle_ticks);
-  return (int)hipGetLastError();
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) {
+      const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (a != hipSuccess) return (int)a;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(RES_WAVES * 64), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req,
+                       act, gran, gstride, mirror, err, done, idle_ticks);
+    return (int)hipGetLastError();
+  };
+  if (local0 && nf == 8) return go(policy_resident_kernel<8>);
+  if (local0 && nf == 16) return go(policy_resident_kernel<16>);
+  return go(policy_resident_kernel<0>);
 }
 
 }  // namespace go2pi

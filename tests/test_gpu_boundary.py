@@ -18,12 +18,15 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
+@pytest.mark.parametrize("resident", ["100", "0"])
 @pytest.mark.parametrize("mode", ["zeros", "twos"])
-def test_cpp_onnx_actor_known_answers(mode):
+def test_cpp_onnx_actor_known_answers(mode, resident):
     """tests/cpp/controller_shape.cpp: make_unique<ONNXActor>(path, std::array<float,98>&,
-    std::array<float,12>&), print_model_info(), act() — as controller.cpp:25,49,215."""
+    std::array<float,12>&), print_model_info(), act() — as controller.cpp:25,49,215.
+    The shim's resident kernel (default) and one launch per call (GO2PI_RESIDENT_MS=0)."""
     exe = build_controller_shape()
-    r = subprocess.run([exe, SHIPPED, mode], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, SHIPPED, mode], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, GO2PI_RESIDENT_MS=resident))
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.splitlines()
     assert lines[:5] == ["Input dimension: 98", "Output dimension: 12", "Input name: observation",
@@ -33,9 +36,11 @@ def test_cpp_onnx_actor_known_answers(mode):
     assert rel_err(act, want) <= TOL
 
 
-def test_cpp_onnx_actor_ticks():
+@pytest.mark.parametrize("resident", ["100", "0"])
+def test_cpp_onnx_actor_ticks(resident):
     exe = build_controller_shape()
-    r = subprocess.run([exe, SHIPPED, "ticks", "500"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, SHIPPED, "ticks", "500"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, GO2PI_RESIDENT_MS=resident))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "best_us:" in r.stdout
 

@@ -1,10 +1,11 @@
 """GPU: the resident batch <= 8 act() path (opts.resident_ms > 0, resident.hip).
 
 One launch serves every go2pi_run at batch <= 8: the observation and the
-request header travel as {epoch, value} granules in host-mapped memory. The
-layers are policy_latency_kernel's, so the resident path must be BIT-identical
-to the one-launch-per-call path (and within the 1e-5 contract of the fp64
-oracle). Also covered: the kernel leaving on idle (a request racing that exit is
+request header travel as {epoch, value} granules in host-mapped memory. Layers
+1.. are policy_latency_kernel's; layer 0 is computed by every workgroup for
+itself (one fma chain per output), so the resident path matches the
+one-launch-per-call path within the 1e-5 contract of the fp64 oracle, and is
+bit-identical to it with GO2PI_RES_TILED0=1 (layer 0 tiled like the others). Also covered: the kernel leaving on idle (a request racing that exit is
 served by a relaunch), another engine call in between (the kernel is stopped
 and relaunched), and destroy while resident.
 """
@@ -24,10 +25,13 @@ def _models(synth_path):
     return {"shipped": SHIPPED, "mlp512": synth_path("go2_mlp_512")}
 
 
+@pytest.mark.parametrize("tiled0", [False, True])
 @pytest.mark.parametrize("name", ["shipped", "mlp512"])
-def test_resident_bitwise_vs_launch_per_call(synth_path, name):
+def test_resident_vs_launch_per_call(synth_path, name, tiled0, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import mlp_ref
+    if tiled0:
+        monkeypatch.setenv("GO2PI_RES_TILED0", "1")  # read at each resident launch
     path = _models(synth_path)[name]
     ref = mlp_ref.MlpRef.from_onnx(path)
     with Engine(path, max_batch=64, resident_ms=500) as r, Engine(path, max_batch=64) as p:
@@ -37,7 +41,12 @@ def test_resident_bitwise_vs_launch_per_call(synth_path, name):
                  else rng.standard_normal((B, r.in_dim)).astype(np.float32))
             y = r.run(x)
             assert y.shape == (B, r.out_dim)
-            assert np.array_equal(y, p.run(x)), f"call {i} B={B}: resident != launch-per-call"
+            assert np.array_equal(y, r.run(x)), f"call {i} B={B}: resident path not deterministic"
+            yp = p.run(x)
+            if tiled0:
+                assert np.array_equal(y, yp), f"call {i} B={B}: resident (tiled layer 0) != launch-per-call"
+            else:
+                assert abs_err(y, yp) <= TOL
             assert abs_err(y, ref.f64(x)) <= TOL
 
 
@@ -110,3 +119,16 @@ def test_resident_two_engines(synth_path):
             xb = rng.standard_normal((2, 48)).astype(np.float32)
             assert abs_err(a.run(xa), ra.f64(xa)) <= TOL
             assert abs_err(b.run(xb), rb.f64(xb)) <= TOL
+
+
+def test_resident_prologue_epilogue(synth_path):
+    """The optional normalisation prologue and tanh/clip/scale epilogue (go2pi_opts) on the resident path."""
+    from go2_onnx_controller_amd import Engine
+    path = synth_path("go2_mlp_512")
+    rng = np.random.default_rng(9)
+    kw = dict(obs_mean=rng.normal(0, 0.3, 48).astype(np.float32), obs_std=rng.uniform(0.5, 2, 48).astype(np.float32),
+              obs_clip=3.0, action_tanh=True, action_clip=0.8, action_scale=0.25, max_batch=8)
+    with Engine(path, resident_ms=500, **kw) as r, Engine(path, **kw) as p:
+        for B in (1, 2, 8, 1):
+            x = rng.normal(0, 2, (B, 48)).astype(np.float32)
+            assert abs_err(r.run(x), p.run(x)) <= TOL

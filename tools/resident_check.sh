@@ -6,6 +6,7 @@ tail -3 gpurun_out/resident_tests.log
 for m in go2_mlp_512 shipped; do
   timeout -k 10 120 python3 tools/latency_probe.py --model $m --iters 5000 || exit 1
   timeout -k 10 120 python3 tools/latency_probe.py --model $m --iters 5000 --resident-ms 200 || exit 1
+  GO2PI_RES_TILED0=1 timeout -k 10 120 python3 tools/latency_probe.py --model $m --iters 5000 --resident-ms 200 || exit 1
 done
 timeout -k 10 120 python3 tools/latency_probe.py --model go2_mlp_512 --iters 5000 --resident-ms 200 --batch 8 || exit 1
 timeout -k 10 120 python3 tools/latency_probe.py --model go2_mlp_512 --iters 5000 --batch 8 || exit 1
