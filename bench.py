@@ -160,27 +160,30 @@ def controller_leg(device, steps=200, warm=20, iters=3000):
         out["tick_us"] = round(tick_us, 3)
         out["policy_only_us"] = round(policy_us, 3)
         out["robot_ticks_per_s"] = round(B / (tick_us * 1e-6), 1)
-    with Engine(path, device=device, max_batch=8) as e:
-        st1, joy1 = (np.ascontiguousarray(t.numpy()) for t in states(1))
-        obs1 = np.zeros((1, e.in_dim), np.float32)
-        act1 = np.zeros((1, 12), np.float32)
-        bufs = [np.empty((1, 12)), np.empty((1, 12)), np.empty((1, 12)), np.empty(1, np.uint32)]
-        fn = lib().go2pi_controller_step
-        args = (e._h, st1.ctypes.data, joy1.ctypes.data, obs1.ctypes.data, act1.ctypes.data,
-                *[b.ctypes.data for b in bufs], 1)
-        ts = []
-        for i in range(warm * 10 + iters):
-            st1[0, 4 + i % 3] = 0.01 * (i % 7)
-            t0 = time.perf_counter_ns()
-            rc = fn(*args)
-            t1 = time.perf_counter_ns()
-            if rc:
-                raise RuntimeError(lib().go2pi_last_error().decode())
-            if i >= warm * 10:
-                ts.append((t1 - t0) / 1e3)
-        ts.sort()
-        out["b1_tick_p50_us"] = round(ts[len(ts) // 2], 2)
-        out["b1_tick_p99_us"] = round(ts[int(len(ts) * 0.99)], 2)
+    # batch-1 host tick: the resident kernel (go2pi_opts.resident_ms, as the ONNXActor shim
+    # uses for act()), then one launch per tick
+    for key, res_ms in (("b1_tick", 100), ("b1_tick_launch", 0)):
+        with Engine(path, device=device, max_batch=8, resident_ms=res_ms) as e:
+            st1, joy1 = (np.ascontiguousarray(t.numpy()) for t in states(1))
+            obs1 = np.zeros((1, e.in_dim), np.float32)
+            act1 = np.zeros((1, 12), np.float32)
+            bufs = [np.empty((1, 12)), np.empty((1, 12)), np.empty((1, 12)), np.empty(1, np.uint32)]
+            fn = lib().go2pi_controller_step
+            args = (e._h, st1.ctypes.data, joy1.ctypes.data, obs1.ctypes.data, act1.ctypes.data,
+                    *[b.ctypes.data for b in bufs], 1)
+            ts = []
+            for i in range(warm * 10 + iters):
+                st1[0, 4 + i % 3] = 0.01 * (i % 7)
+                t0 = time.perf_counter_ns()
+                rc = fn(*args)
+                t1 = time.perf_counter_ns()
+                if rc:
+                    raise RuntimeError(lib().go2pi_last_error().decode())
+                if i >= warm * 10:
+                    ts.append((t1 - t0) / 1e3)
+            ts.sort()
+            out[f"{key}_p50_us"] = round(ts[len(ts) // 2], 2)
+            out[f"{key}_p99_us"] = round(ts[int(len(ts) * 0.99)], 2)
     return out
 
 

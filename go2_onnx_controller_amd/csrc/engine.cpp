@@ -86,6 +86,7 @@ struct go2pi_engine {
   unsigned epoch = 1, last_epoch = 0;
   // resident batch <= SMALL_MAXB path (resident.hip, opts.resident_ms > 0)
   bool resident_ok = false, resident_live = false;
+  bool resident_ctl = false;  // the live kernel is the controller-tick form
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
   unsigned long long *d_mirror = nullptr;                 // device copy of the request (workgroup 0 -> the rest)
   unsigned long long res_idle_ticks = 0;                  // 100 MHz wall-clock ticks
@@ -172,7 +173,7 @@ struct go2pi_engine {
     resident_live = false;
     hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize (resident kernel leaving)");
   }
-  void resident_start() {
+  void resident_start(const go2pi::DevCtl *ctl) {
     const size_t ng = (size_t)std::max(1, prog.nl - 1) * gstride;
     hip_check(hipMemsetAsync(d_gran, 0, ng * sizeof(unsigned long long), stream), "hipMemsetAsync");
     hip_check(hipMemsetAsync(d_mirror, 0, sizeof(unsigned long long) * (1 + GO2PI_SMALL_MAXB * (size_t)model.in_dim),
@@ -181,14 +182,18 @@ struct go2pi_engine {
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_act, d_gran, gstride, d_mirror, m_err, m_done,
-                                     res_idle_ticks, stream),
+                                     res_idle_ticks, ctl, stream),
               "resident launch");
     resident_live = true;
+    resident_ctl = ctl != nullptr;
     res_last = std::chrono::steady_clock::now();
   }
-  // obs/act: host rows [batch][in_dim] / [batch][out_dim]
-  void resident_run(const float *obs, float *act, int64_t batch) {
-    const int n = (int)batch * model.in_dim;
+  // One request to the resident kernel. ctl null: act(), obs = host rows [batch][in_dim]
+  // (sent as tagged granules), the action lands in h_act. ctl: a controller tick whose
+  // rows the caller has written to the staging ctl names; flags = GO2PI_RES_* bits.
+  void resident_serve(const go2pi::DevCtl *ctl, const float *obs, int64_t batch, unsigned flags) {
+    if (resident_live && resident_ctl != (ctl != nullptr)) resident_stop();  // the other form is live
+    const int n = ctl ? 0 : (int)batch * model.in_dim;
     const auto idle = std::chrono::milliseconds(opts.resident_ms);
     for (int attempt = 0;; ++attempt) {
       // layer tags e + 1 + l: an epoch spans nl + 2 tags
@@ -204,13 +209,13 @@ struct go2pi_engine {
       // the kernel leaves after resident_ms idle: past half of it, relaunch rather than race its exit
       if (resident_live && (now - res_last > idle / 2 || __atomic_load_n(h_done, __ATOMIC_ACQUIRE) == GO2PI_RES_LEAVE))
         resident_stop();
-      if (!resident_live) resident_start();
+      if (!resident_live) resident_start(ctl);
       for (int i = 0; i < n; ++i) {
         unsigned bits;
         std::memcpy(&bits, obs + i, 4);
         __atomic_store_n(h_req + 1 + i, ((unsigned long long)e0 << 32) | bits, __ATOMIC_RELAXED);
       }
-      __atomic_store_n(h_req, ((unsigned long long)e0 << 32) | (unsigned)batch, __ATOMIC_RELEASE);
+      __atomic_store_n(h_req, ((unsigned long long)e0 << 32) | (unsigned)batch | flags, __ATOMIC_RELEASE);
       const auto t0 = std::chrono::steady_clock::now();
       unsigned d;
       for (unsigned it = 0; (d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) != e0 && d != GO2PI_RES_LEAVE; ++it) {
@@ -218,10 +223,7 @@ struct go2pi_engine {
         if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
       }
       res_last = std::chrono::steady_clock::now();
-      if (d == e0) {
-        std::memcpy(act, h_act, sizeof(float) * (size_t)batch * model.out_dim);
-        return;
-      }
+      if (d == e0) return;
       // the kernel left (idle exit racing this request, or a hand-off timeout): wait for
       // it to drain, then serve the request from a fresh launch with a fresh epoch
       resident_stop();
@@ -726,8 +728,9 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
     if (!obs || !act) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     if (e->resident_ok && batch <= GO2PI_SMALL_MAXB) {
-      e->resident_run(obs, act, batch);
+      e->resident_serve(nullptr, obs, batch, 0u);
       e->check_handoff();
+      std::memcpy(act, e->h_act, sizeof(float) * (size_t)batch * e->model.out_dim);
       return GO2PI_OK;
     }
     e->resident_stop();
@@ -968,10 +971,26 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
     c.kp = kp ? reinterpret_cast<double *>(dev + L.kp) : nullptr;
     c.kd = kd ? reinterpret_cast<double *>(dev + L.kd) : nullptr;
     c.status = status ? reinterpret_cast<uint32_t *>(dev + L.status) : nullptr;
-    const bool single = small && e->use_latency(batch) && e->done_ok;
-    e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
+    const bool res = small && e->resident_ok && e->done_ok;
+    if (res) {
+      // the resident kernel's controller form: every optional row has its place in the
+      // staging; the header's flags say which this call passed
+      go2pi::DevCtl all = c;
+      all.joy = reinterpret_cast<const float *>(dev + L.joy);
+      all.q_des = reinterpret_cast<double *>(dev + L.q_des);
+      all.kp = reinterpret_cast<double *>(dev + L.kp);
+      all.kd = reinterpret_cast<double *>(dev + L.kd);
+      all.status = reinterpret_cast<uint32_t *>(dev + L.status);
+      const unsigned flags = (joy ? GO2PI_RES_JOY : 0u) | (q_des ? GO2PI_RES_QDES : 0u) | (kp ? GO2PI_RES_KP : 0u) |
+                             (kd ? GO2PI_RES_KD : 0u) | (status ? GO2PI_RES_STATUS : 0u);
+      e->resident_serve(&all, nullptr, batch, flags);
+    } else {
+      e->resident_stop();
+    }
+    const bool single = !res && small && e->use_latency(batch) && e->done_ok;
+    if (!res) e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
     if (small) {
-      const bool synced = single && e->spin_done();
+      const bool synced = res || (single && e->spin_done());
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
       e->check_handoff();
       std::memcpy(obs, e->h_ctl + L.obs, n_obs);

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "ctl_fn.hpp"
 #include "device_fn.hpp"
 #include "program.hpp"
 
@@ -76,269 +77,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 #else
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// Controller tick. The observation is the concatenation
-// of seven history blocks (controller.cpp:210-212); block b holds kHistory
-// copies of a d_b-wide signal, oldest first, and each tick shifts it left by
-// d_b and appends the current value (populate_buffer, controller.hpp:45-52).
-// Blocks: gravity_b 3, base_ang_vel 3, vel_cmd 3, q - q0 12, dq 12, previous
-// action 12, foot contacts 4 (49 per step).
-
-// gravity_b = quaternion_.inverse() * gravity_w_ (controller.cpp:182-184) with
-// Eigen 3.4 semantics: inverse() = conjugate / squaredNorm (the zero quaternion
-// if squaredNorm <= 0), squaredNorm summed as (x²+z²)+(y²+w²) (SSE predux of
-// the (x,y,z,w) coefficients), and q * v = _transformVector:
-// uv = 2 (q.vec × v), r = (v + w uv) + q.vec × uv. Every operation rounds to
-// fp32 in that order (no fma contraction), like the reference's x86 build.
-__device__ __forceinline__ float ctl_gravity(const float *st, float v0, float v1, float v2, int i) {
-#pragma clang fp contract(off)
-  const float w = st[0], x = st[1], y = st[2], z = st[3];
-  const float n2 = (x * x + z * z) + (y * y + w * w);
-  float qw = 0.f, qx = 0.f, qy = 0.f, qz = 0.f;
-  if (n2 > 0.f) {
-    qx = -x / n2;
-    qy = -y / n2;
-    qz = -z / n2;
-    qw = w / n2;
-  }
-  float u0 = qy * v2 - qz * v1, u1 = qz * v0 - qx * v2, u2 = qx * v1 - qy * v0;
-  u0 += u0;
-  u1 += u1;
-  u2 += u2;
-  const float c0 = qy * u2 - qz * u1, c1 = qz * u0 - qx * u2, c2 = qx * u1 - qy * u0;
-  if (i == 0) return (v0 + qw * u0) + c0;
-  if (i == 1) return (v1 + qw * u1) + c1;
-  return (v2 + qw * u2) + c2;
-}
-
-// Direct-to-LDS copy of n contiguous floats (global_load_lds_dword: no VGPR
-// round trip, every load of the workgroup in flight at once). dst needs room
-// for ceil64(n) floats (the tail lanes re-read element n-1). Complete after
-// the next __syncthreads() (its fence waits vmcnt(0)).
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-// Before the barrier that hands LDS-DMA'd bytes to OTHER waves, each issuing wave
-// waits for its own direct-to-LDS loads: the compiler's barrier fence does not
-// count them (MI355X_MICROARCH.md §Two waves per SIMD, item 7: nothing orders a
-// ds_read behind a pending LDS-DMA except the issuing wave's covering vmcnt).
-__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// Workgroup barrier that leaves this wave's N youngest vector-memory ops in flight
-// (weight fragments prefetched for after the barrier); __syncthreads()'s fence
-// would wait for all of them. Everything older — the LDS-DMA the barrier publishes
-// — has landed: loads return in issue order. The caller keeps exactly N loads
-// between the DMA and this barrier (compiler barriers on both sides).
-template <int N>
-__device__ __forceinline__ void wg_barrier_vm() {
-  static_assert(N >= 0 && N <= 63, "vmcnt immediate");
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ void glds_copy(float *dst, const float *src, int n, int wave, int lane, int nw) {
-  for (int base = wave * 64; base < n; base += nw * 64) {
-    const int i = min(base + lane, n - 1);
-    __builtin_amdgcn_global_load_lds((gvoid_t *)(src + i), (lvoid_t *)(dst + base), 4, 0, 0);
-  }
-}
-
-// LDS image of one tile's controller inputs (rows r < R of the tile): q0
-// (double), raw state rows, joystick rows, previous action / observation rows,
-// per-row NaN flags. Plain values passed by value (no address-taken locals:
-// nothing spills to scratch).
-struct CtlLds {
-  double *q0;
-  float *st, *jy, *act, *obs;
-  unsigned *nanf;
-};
-
-__host__ __device__ inline int ctl_lds_floats(int R, int in_dim) {
-  auto c64 = [](int x) { return (x + 63) & ~63; };
-  return 24 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) + c64(R * in_dim) +
-         GO2PI_TILE_ROWS;
-}
-
-__device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim) {
-  auto c64 = [](int x) { return (x + 63) & ~63; };
-  CtlLds L;
-  L.q0 = reinterpret_cast<double *>(base);
-  L.st = base + 24;
-  L.jy = L.st + c64(R * GO2PI_CTL_STATE_DIM);
-  L.act = L.jy + c64(R * GO2PI_CTL_JOY_DIM);
-  L.obs = L.act + c64(R * GO2PI_CTL_DOF);
-  L.nanf = reinterpret_cast<unsigned *>(L.obs + c64(R * in_dim));
-  return L;
-}
-
-// Issue the direct-to-LDS loads of rows [row0, row0 + nrows) and clear the NaN flags.
-__device__ __forceinline__ void ctl_lds_load(const CtlLds L, const DevCtl C, int row0, int nrows, int in_dim, int tid,
-                                             int wave, int lane, int nw) {
-  glds_copy(L.st, C.state + (size_t)row0 * GO2PI_CTL_STATE_DIM, nrows * GO2PI_CTL_STATE_DIM, wave, lane, nw);
-  if (C.joy) glds_copy(L.jy, C.joy + (size_t)row0 * GO2PI_CTL_JOY_DIM, nrows * GO2PI_CTL_JOY_DIM, wave, lane, nw);
-  glds_copy(L.act, C.action + (size_t)row0 * GO2PI_CTL_DOF, nrows * GO2PI_CTL_DOF, wave, lane, nw);
-  glds_copy(L.obs, C.obs + (size_t)row0 * in_dim, nrows * in_dim, wave, lane, nw);
-  if (tid < GO2PI_CTL_DOF) L.q0[tid] = C.prm->q0[tid];
-  if (tid < GO2PI_TILE_ROWS) L.nanf[tid] = 0u;
-}
-
-// Controller parameters the assembly reads, loaded once at kernel start (by
-// value: their scalar loads overlap the input staging instead of following it).
-struct CtlQ {
-  int hist;
-  float thr, g0, g1, g2;
-};
-
-__device__ __forceinline__ CtlQ ctl_q(const DevCtl C) {
-  const DevCtlParams &Q = *C.prm;
-  return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2]};
-}
-
-// One history block BK of the new observation rows r < nrows, on one wave's
-// lanes: straight-line code per block (BK is a template parameter).
-template <int BK, bool TILE>
-__device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
-                                               float *dst, int ds, float *raw, int lane, int stride = 64) {
-  constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
-  constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
-  const int H = q.hist, in_dim = P.in_dim;
-  const int W = H * d, s0 = H * cum, sh = (H - 1) * d;
-  const float rW = 1.f / (float)W;
-#pragma unroll 2
-  for (int e = lane; e < nrows * W; e += stride) {
-    // r = e / W exactly: (e + 0.5) / W is >= 0.5 / W away from an integer and the
-    // float product's error is far below that for these sizes (W <= 49 * 16)
-    const int r = (int)(((float)e + 0.5f) * rW);
-    const int j = e - r * W, k = s0 + j;
-    const float *orow = L.obs + r * in_dim;
-    float v;
-    if (j < sh) {
-      v = orow[k + d];  // std::shift_left by d
-    } else {
-      const int i = j - sh;
-      const float *st = L.st + r * GO2PI_CTL_STATE_DIM;
-      if constexpr (BK == 0) {
-        v = ctl_gravity(st, q.g0, q.g1, q.g2, i);
-      } else if constexpr (BK == 1) {
-        v = st[4 + i];  // imu gyroscope (controller.hpp:105-109)
-      } else if constexpr (BK == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
-        const float *jy = L.jy + r * GO2PI_CTL_JOY_DIM;
-        if (!joy || jy[0] == 0.f) v = orow[k];  // the previous tick's vel_cmd_
-        else if (i == 0) v = jy[2];             // axes[1]
-        else if (i == 2) v = jy[3] * jy[2];     // axes[3] * axes[1]
-        else {                                  // pow(axes[0], 2) * sign * 0.8 in double
-          const double a0 = jy[1];
-          v = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
-        }
-      } else if constexpr (BK == 3) {
-        v = (float)((double)st[7 + i] - L.q0[i]);  // q_[i] -= q0_[i] (double q0_)
-      } else if constexpr (BK == 4) {
-        v = st[19 + i];
-      } else if constexpr (BK == 5) {
-        v = L.act[r * GO2PI_CTL_DOF + i];  // action_ before act()
-      } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
-        v = st[31 + (i ^ 1)] >= q.thr ? 1.f : 0.f;
-      }
-      if (BK < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
-    }
-    if (raw) raw[r * in_dim + k] = v;
-    dst[r * ds + k] = TILE ? prologue(P, v, k) : v;
-  }
-}
-
-// Assemble this tick's observation rows r < nrows from the LDS image: one job
-// per history block spread over the waves (each wave runs one block's
-// straight-line code), plus — TILE: dst is the batched kernel's LDS tile — a
-// job zeroing its padding columns [in_dim, in_pad) and rows [nrows, 16).
-// Per element: the raw value goes to raw[r * in_dim + k] (the tile's global
-// obs rows; may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k].
-// NaN among the appended values of blocks 0-5 — where the reference's
-// populate_buffer check exit(1)s (controller.hpp:57-64) — sets nanf[r].
-// Needs the image complete (barrier).
-template <bool TILE>
-__device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
-                                             float *dst, int ds, float *raw, int wave, int lane, int nw) {
-  for (int job = wave; job < 8; job += nw) {
-    switch (job) {
-      case 0: ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 1: ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 2: ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 3: ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 4: ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 5: ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 6: ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      default:
-        if constexpr (TILE) {  // padding
-          const int in_dim = P.in_dim, pw = P.in_pad - in_dim;
-          const float rp = 1.f / (float)pw;
-          for (int e = lane; e < nrows * pw; e += 64) {
-            const int r = (int)(((float)e + 0.5f) * rp);
-            dst[r * ds + in_dim + (e - r * pw)] = 0.f;
-          }
-          for (int r = nrows; r < GO2PI_TILE_ROWS; ++r)
-            for (int k = lane; k < P.in_pad; k += 64) dst[r * ds + k] = 0.f;
-        }
-        break;
-    }
-  }
-}
-
-// The same assembly with every block spread over ALL the workgroup's threads
-// (thread t, stride nt), the blocks one after another: at 4 waves per workgroup
-// the one-job-per-wave split left each wave two whole blocks in series
-// (measured 9.6K cycles for the tile, against ~4K at 8 waves).
-template <bool TILE>
-__device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
-                                                  int nrows, float *dst, int ds, float *raw, int tid, int nt) {
-  ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  if constexpr (TILE) {  // padding columns [in_dim, in_pad) and rows [nrows, 16)
-    const int in_dim = P.in_dim, pw = P.in_pad - in_dim;
-    const float rp = 1.f / (float)pw;
-    for (int e = tid; e < nrows * pw; e += nt) {
-      const int r = (int)(((float)e + 0.5f) * rp);
-      dst[r * ds + in_dim + (e - r * pw)] = 0.f;
-    }
-    for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * P.in_pad; e += nt) {
-      const int r = nrows + e / P.in_pad;
-      dst[r * ds + (e - (r - nrows) * P.in_pad)] = 0.f;
-    }
-  }
-}
-
-// What the final layer's store needs (controller tick), by value: the call's
-// output pointers, the parameters, and this tile's LDS q0 / joystick rows.
-struct CtlView {
-  float *action;
-  double *q_des, *kp, *kd;
-  const double *q0;
-  const float *jy;  // null: no joystick
-  double scale, kp_run, kp_stop, kd_run;
-  float lim;
-  int row0;
-  int on;  // 0: plain policy launch (the final layer writes `out`)
-};
-
-__device__ __forceinline__ CtlView ctl_view(const DevCtl C, const CtlLds L, int row0) {
-  const DevCtlParams &Q = *C.prm;
-  return CtlView{C.action, C.q_des, C.kp, C.kd, L.q0, C.joy ? L.jy : nullptr, Q.action_scale, Q.kp_run,
-                 Q.kp_stop, Q.kd_run, Q.action_limit, row0, 1};
-}
-
-// Action post-processing of robot `row`, joint n (controller.cpp:217-223, 240-248).
-__device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float v) {
-  float a = v < -V.lim ? -V.lim : (V.lim < v ? V.lim : v);  // std::clamp (NaN passes through)
-  const bool stop = V.jy && V.jy[(row - V.row0) * GO2PI_CTL_JOY_DIM + 4] != 0.f;
-  a *= stop ? 0.f : 1.f;  // a *= joy_->buttons[0] == 0
-  const size_t o = (size_t)row * GO2PI_CTL_DOF + n;
-  V.action[o] = a;
-  if (V.q_des) V.q_des[o] = V.q0[n] + (double)a * V.scale;
-  if (V.kp) V.kp[o] = stop ? V.kp_stop : V.kp_run;
-  if (V.kd) V.kd[o] = V.kd_run;
 }
 
 // ---------------------------------------------------------------------------

@@ -134,10 +134,18 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 // epoch + 1 + l. gran must be zeroed before every launch (a leaving workgroup tags
 // its slots GO2PI_RES_LEAVE so waiting consumers leave too). mirror: device
 // [1 + SMALL_MAXB * in_dim] granules, workgroup 0's copy of each request for the
-// other workgroups (zeroed before every launch, like gran).
+// other workgroups (zeroed before every launch, like gran). ctl non-null: the
+// controller-tick form (go2pi_controller_step at batch <= 8): ctl's rows are the
+// pinned host staging, req[0] = {epoch, batch | GO2PI_RES_* flags} only.
 #define GO2PI_RES_LEAVE 0xFFFFFFFFu
+// Controller-tick request flags (header low word, bits 8..): the optional rows the call passed.
+#define GO2PI_RES_JOY (1u << 8)
+#define GO2PI_RES_QDES (1u << 9)
+#define GO2PI_RES_KP (1u << 10)
+#define GO2PI_RES_KD (1u << 11)
+#define GO2PI_RES_STATUS (1u << 12)
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
-                    unsigned *done, unsigned long long idle_ticks, void *stream);
+                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, void *stream);
 
 }  // namespace go2pi

@@ -34,6 +34,7 @@
 
 #include <cstdlib>
 
+#include "ctl_fn.hpp"
 #include "device_fn.hpp"
 #include "program.hpp"
 
@@ -87,7 +88,8 @@ __device__ __forceinline__ int sweep(const u64 *g, int n, unsigned tag, float *d
 // of the 100 MHz wall clock without a request.
 template <int SCOPE>
 __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned last, u64 idle_ticks, float *obsv,
-                                             unsigned *err, int lane, int &leave, unsigned &e, int &B) {
+                                             unsigned *err, int lane, int &leave, unsigned &e, int &B,
+                                             unsigned &word) {
   u64 *qm = const_cast<u64 *>(q);
   const u64 t0 = wall_clock64();
   const int npoll = min(1 + in_dim, 64 * RES_POLL);
@@ -105,7 +107,8 @@ __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned 
     }
     if (tag != 0u && tag != last) {
       e = tag;
-      B = min(max((int)(unsigned)h, 1), GO2PI_SMALL_MAXB);
+      word = (unsigned)h;
+      B = min(max((int)(word & 0xFFu), 1), GO2PI_SMALL_MAXB);
       const int n = B * in_dim;  // observation granules q[1 .. n]
       if (1 + n <= npoll) {
         bool ok = true;
@@ -196,11 +199,16 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
 
 // NF > 0: local layer 0 (above) with NF fragments per thread; 0: layer 0 tiled
 // over the workgroups like every other layer (policy_latency_kernel's order).
-template <int NF>
+// CTL: the controller tick (go2pi_controller_step at batch <= 8): workgroup 0
+// reads the tick's raw rows from the host staging named by `C` once the header
+// arrives, assembles the observation (ctl_fn.hpp, as policy_latency_ctl_kernel),
+// mirrors it, and post-processes the action into the staging (ctl_store); the
+// header's low word carries the batch and GO2PI_RES_* flags.
+template <int NF, bool CTL>
 __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
                                                                          const u64 *req, float *act, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
-                                                                         unsigned *done, u64 idle_ticks) {
+                                                                         unsigned *done, u64 idle_ticks, DevCtl C) {
   constexpr bool LOCAL0 = NF > 0;
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
@@ -210,6 +218,11 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   float *obsv = reinterpret_cast<float *>(st + 4);                   // [B][in_dim] the request's observation
   float *x0 = obsv + GO2PI_SMALL_MAXB * P.in_dim;                    // LOCAL0: [B][K0] prologued layer-0 input
   float *p0 = x0 + GO2PI_SMALL_MAXB * P.L[0].K_pad;                  // LOCAL0, KS > 1: [KS][B][N0] partials
+  // CTL: the LDS image of the tick's inputs (16-byte aligned: q0 is double)
+  // (p0's size: KS * MAXB * N0 floats when 512 / N0 = KS > 1 slices, as launch_resident reserves)
+  const int ks0 = ((RES_WAVES * 64) % P.L[0].N_pad == 0 && P.L[0].N_pad < RES_WAVES * 64) ? (RES_WAVES * 64) / P.L[0].N_pad : 0;
+  float *cbase = p0 + (ks0 * GO2PI_SMALL_MAXB * P.L[0].N_pad + 3) / 4 * 4;
+  const CtlLds CL = ctl_lds(cbase, GO2PI_SMALL_MAXB, P.in_dim);
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
@@ -259,31 +272,69 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     // host memory over PCIe while idle.
     if (wave == 0) {
       int leave = 0, B = 0;
-      unsigned e = 0;
+      unsigned e = 0, word = 0;
       if (g == 0) {
-        wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B);
-        const int n = leave ? 0 : B * in_dim;
+        // CTL: the header alone (the rows are plain floats in the staging)
+        wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, CTL ? 0 : in_dim, last, idle_ticks, obsv, err, lane, leave, e, B,
+                                                word);
+        const int n = (leave || CTL) ? 0 : B * in_dim;
         for (int i = lane; i < n; i += 64)
           __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0)
+        if (lane == 0 && (leave || !CTL))
           __hip_atomic_store(mirror, leave ? ((u64)GO2PI_RES_LEAVE << 32) : (((u64)e << 32) | (unsigned)B),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        wait_request<__HIP_MEMORY_SCOPE_AGENT>(mirror, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B);
+        wait_request<__HIP_MEMORY_SCOPE_AGENT>(mirror, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word);
       }
       if (lane == 0) {
         st[0] = leave;
         st[1] = (int)e;
         st[2] = B;
+        st[3] = (int)word;
       }
     }
     __syncthreads();
     if (st[0]) break;
     const unsigned e = (unsigned)st[1];
     const int B = st[2];
+    const unsigned word = (unsigned)st[3];
     last = e;
     bool left = false;
+    CtlView cv{};
+    if constexpr (CTL) {
+      if (g == 0) {
+        // the tick's raw rows from host memory (system scope: fresh every request)
+        const bool joy = (word & GO2PI_RES_JOY) != 0u;
+        auto fetch = [&](float *dst, const float *src, int cnt) {
+          for (int i = tid; i < cnt; i += RES_WAVES * 64)
+            dst[i] = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned *>(const_cast<float *>(src)) + i,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        };
+        fetch(CL.st, C.state, B * GO2PI_CTL_STATE_DIM);
+        if (joy) fetch(CL.jy, C.joy, B * GO2PI_CTL_JOY_DIM);
+        fetch(CL.act, C.action, B * GO2PI_CTL_DOF);
+        fetch(CL.obs, C.obs, B * in_dim);
+        if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
+        if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
+        __syncthreads();
+        ctl_assemble_flat<false>(P, CL, ctl_q(C), joy, B, obsv, in_dim, nullptr, tid, RES_WAVES * 64);
+        __syncthreads();
+        if (wave == 0) {  // mirror the assembled observation for the other workgroups
+          for (int i = lane; i < B * in_dim; i += 64)
+            __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0)
+            __hip_atomic_store(mirror, ((u64)e << 32) | (unsigned)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        DevCtl c = C;
+        if (!joy) c.joy = nullptr;
+        if (!(word & GO2PI_RES_QDES)) c.q_des = nullptr;
+        if (!(word & GO2PI_RES_KP)) c.kp = nullptr;
+        if (!(word & GO2PI_RES_KD)) c.kd = nullptr;
+        cv = ctl_view(c, CL, 0);
+      }
+    }
 
     // ---- the layers (policy_latency_kernel's body; tags e + 1 + l)
     if constexpr (LOCAL0) local_layer0<NF>(P, w0, b0, obsv, x0, p0, xs, B, tid);
@@ -355,8 +406,12 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           for (int w2 = 0; w2 < RES_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
           const float v = act_fn(L.act, L.alpha, s + bcur);
           if (lastl) {
-            if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
-            if (b == B - 1 && g == 0) {
+            if constexpr (CTL) {
+              if (n < L.N) ctl_store(cv, b, n, post_fn(P, v));
+            } else {
+              if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
+            }
+            if (!CTL && b == B - 1 && g == 0) {
               // every action store of this tile drained and system-visible before the done word
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -372,6 +427,16 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       __syncthreads();  // xs / part reused by the next layer
     }
     if (left) break;
+    if constexpr (CTL) {
+      if (g == 0) {  // the new observation rows and NaN flags, then the done word
+        for (int i = tid; i < B * in_dim; i += RES_WAVES * 64) C.obs[i] = obsv[i];
+        if ((word & GO2PI_RES_STATUS) && tid < B) C.status[tid] = CL.nanf[tid];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
   // ---- leave: consumers still waiting on this workgroup's slots leave too
   tag_leave(P, gran, gstride, g, tid, LOCAL0 ? 1 : 0);
@@ -385,7 +450,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
 
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
-                    unsigned *done, unsigned long long idle_ticks, void *stream) {
+                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, void *stream) {
   if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
   int grid = 1;
   for (int l = 0; l < p.nl; ++l) {
@@ -397,9 +462,11 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   const int KS = (N0 > 0 && (RES_WAVES * 64) % N0 == 0) ? (RES_WAVES * 64) / N0 : 0;
   const int nf = (KS > 0 && C0 % KS == 0) ? 4 * (C0 / KS) : 0;
   const bool local0 = p.nl >= 2 && (nf == 8 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
-  const size_t lds = sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 +
-                                      4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim +
-                                      (local0 ? (size_t)GO2PI_SMALL_MAXB * (p.L[0].K_pad + (KS > 1 ? KS * N0 : 0)) : 0));
+  // (the kernel's LDS carve-up: x0 and p0 are laid out whether used or not)
+  const size_t ctl_off = ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
+                          (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * p.L[0].K_pad +
+                          (size_t)(KS > 1 ? KS : 0) * GO2PI_SMALL_MAXB * N0 + 3) / 4 * 4;
+  const size_t lds = sizeof(float) * (ctl_off + (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) : 0));
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
@@ -408,12 +475,17 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
       if (a != hipSuccess) return (int)a;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(RES_WAVES * 64), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req,
-                       act, gran, gstride, mirror, err, done, idle_ticks);
+                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{});
     return (int)hipGetLastError();
   };
-  if (local0 && nf == 8) return go(policy_resident_kernel<8>);
-  if (local0 && nf == 16) return go(policy_resident_kernel<16>);
-  return go(policy_resident_kernel<0>);
+  if (ctl) {
+    if (local0 && nf == 8) return go(policy_resident_kernel<8, true>);
+    if (local0 && nf == 16) return go(policy_resident_kernel<16, true>);
+    return go(policy_resident_kernel<0, true>);
+  }
+  if (local0 && nf == 8) return go(policy_resident_kernel<8, false>);
+  if (local0 && nf == 16) return go(policy_resident_kernel<16, false>);
+  return go(policy_resident_kernel<0, false>);
 }
 
 }  // namespace go2pi

@@ -176,3 +176,40 @@ def test_controller_rejects_non_controller_policy(synth_path):
         with pytest.raises(Go2piError):
             e.controller_step(np.zeros((1, 36), np.float32), np.zeros((1, 48), np.float32),
                               np.zeros((1, 12), np.float32))
+
+
+@pytest.mark.parametrize("B", [1, 3, 8])
+def test_controller_ticks_resident(B):
+    """The resident kernel's controller form (go2pi_opts.resident_ms > 0, batch <= 8):
+    same bit-exact observation / action contract, with and without joystick rows,
+    with and without the optional outputs, and switching to and from the act() form."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import controller_ref as cr
+    pol = _mlp_policy(SHIPPED)
+    with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
+        obs, act = _run_ticks(e, pol, B, 6, seed=40 + B)
+        _run_ticks(e, pol, B, 4, seed=50 + B, joy_mode="none")
+        rng = np.random.default_rng(60 + B)
+        for t in range(4):
+            st, joy = cr.synthetic_states(rng, B), cr.synthetic_joy(rng, B)
+            o0, a0 = obs.copy(), act.copy()
+            assert e.controller_step(st, obs, act, joy=joy, outputs=False) is None
+            _check(st, joy, o0, a0, obs, act, None, 2, pol)
+            x = rng.standard_normal((B, 98)).astype(np.float32)  # the act() form in between
+            assert rel_err(e.run(x), pol(x)) <= TOL
+
+
+def test_controller_resident_nan_status():
+    from go2_onnx_controller_amd import Engine
+    from oracle import controller_ref as cr
+    rng = np.random.default_rng(77)
+    B = 4
+    with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
+        st = cr.synthetic_states(rng, B)
+        st[1, 8] = np.nan  # q of robot 1
+        obs = np.zeros((B, 98), np.float32)
+        act = np.zeros((B, 12), np.float32)
+        o0, a0 = obs.copy(), act.copy()
+        _, _, _, status = e.controller_step(st, obs, act)
+        _, want = cr.assemble_obs(o0, a0, st, None, 2)
+        assert np.array_equal(status, want) and status[1] == 1 and status[0] == 0
