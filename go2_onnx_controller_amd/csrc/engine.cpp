@@ -87,6 +87,7 @@ struct go2pi_engine {
   // resident batch <= SMALL_MAXB path (resident.hip, opts.resident_ms > 0)
   bool resident_ok = false, resident_live = false;
   bool resident_ctl = false;  // the live kernel is the controller-tick form
+  std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
   unsigned long long *d_mirror = nullptr;                 // device copy of the request (workgroup 0 -> the rest)
   unsigned long long res_idle_ticks = 0;                  // 100 MHz wall-clock ticks
@@ -188,12 +189,13 @@ struct go2pi_engine {
     resident_ctl = ctl != nullptr;
     res_last = std::chrono::steady_clock::now();
   }
-  // One request to the resident kernel. ctl null: act(), obs = host rows [batch][in_dim]
-  // (sent as tagged granules), the action lands in h_act. ctl: a controller tick whose
-  // rows the caller has written to the staging ctl names; flags = GO2PI_RES_* bits.
-  void resident_serve(const go2pi::DevCtl *ctl, const float *obs, int64_t batch, unsigned flags) {
+  // One request to the resident kernel. ctl null: act(), `rows` = obs [batch][in_dim];
+  // the action lands in h_act. ctl: a controller tick, `rows` = its inputs concatenated
+  // (state | joystick | obs | action, each batch rows); the outputs land in the staging
+  // ctl names; flags = GO2PI_RES_* bits. The rows travel as tagged granules.
+  void resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
     if (resident_live && resident_ctl != (ctl != nullptr)) resident_stop();  // the other form is live
-    const int n = ctl ? 0 : (int)batch * model.in_dim;
+    const int n = (int)batch * (model.in_dim + (ctl ? GO2PI_CTL_RAW : 0));
     const auto idle = std::chrono::milliseconds(opts.resident_ms);
     for (int attempt = 0;; ++attempt) {
       // layer tags e + 1 + l: an epoch spans nl + 2 tags
@@ -212,7 +214,7 @@ struct go2pi_engine {
       if (!resident_live) resident_start(ctl);
       for (int i = 0; i < n; ++i) {
         unsigned bits;
-        std::memcpy(&bits, obs + i, 4);
+        std::memcpy(&bits, rows + i, 4);
         __atomic_store_n(h_req + 1 + i, ((unsigned long long)e0 << 32) | bits, __ATOMIC_RELAXED);
       }
       __atomic_store_n(h_req, ((unsigned long long)e0 << 32) | (unsigned)batch | flags, __ATOMIC_RELEASE);
@@ -544,10 +546,12 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     }
     // resident path: the latency kernel's program shape, the request ring in host memory
     if (e.latency_ok && e.done_ok && e.opts.resident_ms > 0) {
-      hip_check(hipHostMalloc((void **)&e.h_req, sizeof(unsigned long long) * (1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim),
+      // room for a controller tick's rows too (GO2PI_CTL_RAW + in_dim floats per robot)
+      const size_t nreq = 1 + GO2PI_SMALL_MAXB * (size_t)(m.in_dim + GO2PI_CTL_RAW);
+      hip_check(hipHostMalloc((void **)&e.h_req, sizeof(unsigned long long) * nreq,
                               hipHostMallocMapped | hipHostMallocCoherent),
                 "hipHostMalloc");
-      std::memset(e.h_req, 0, sizeof(unsigned long long) * (1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim));
+      std::memset(e.h_req, 0, sizeof(unsigned long long) * nreq);
       hip_check(hipHostGetDevicePointer((void **)&e.m_req, e.h_req, 0), "hipHostGetDevicePointer");
       e.d_mirror = e.dalloc<unsigned long long>(1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim);
       int khz = 0;
@@ -983,7 +987,13 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
       all.status = reinterpret_cast<uint32_t *>(dev + L.status);
       const unsigned flags = (joy ? GO2PI_RES_JOY : 0u) | (q_des ? GO2PI_RES_QDES : 0u) | (kp ? GO2PI_RES_KP : 0u) |
                              (kd ? GO2PI_RES_KD : 0u) | (status ? GO2PI_RES_STATUS : 0u);
-      e->resident_serve(&all, nullptr, batch, flags);
+      float *rows = e->res_rows.data();  // state | joystick | obs | action
+      std::memcpy(rows, state, n_state);
+      if (joy) std::memcpy(rows + batch * GO2PI_CTL_STATE_DIM, joy, n_joy);
+      else std::memset(rows + batch * GO2PI_CTL_STATE_DIM, 0, n_joy);
+      std::memcpy(rows + batch * (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM), obs, n_obs);
+      std::memcpy(rows + batch * (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM + in_dim), action, n_act);
+      e->resident_serve(&all, rows, batch, flags);
     } else {
       e->resident_stop();
     }

@@ -136,9 +136,12 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 // [1 + SMALL_MAXB * in_dim] granules, workgroup 0's copy of each request for the
 // other workgroups (zeroed before every launch, like gran). ctl non-null: the
 // controller-tick form (go2pi_controller_step at batch <= 8): ctl's rows are the
-// pinned host staging, req[0] = {epoch, batch | GO2PI_RES_* flags} only.
+// pinned host staging of the outputs; req[0] = {epoch, batch | GO2PI_RES_* flags},
+// req[1 ..] = the tick's rows as {epoch, value} granules: state [B][36], joystick
+// [B][5], previous obs [B][in_dim], previous action [B][12].
 #define GO2PI_RES_LEAVE 0xFFFFFFFFu
 // Controller-tick request flags (header low word, bits 8..): the optional rows the call passed.
+#define GO2PI_CTL_RAW (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM + GO2PI_CTL_DOF)  // request floats per robot + in_dim
 #define GO2PI_RES_JOY (1u << 8)
 #define GO2PI_RES_QDES (1u << 9)
 #define GO2PI_RES_KP (1u << 10)

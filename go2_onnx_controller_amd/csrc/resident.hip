@@ -86,18 +86,18 @@ __device__ __forceinline__ int sweep(const u64 *g, int n, unsigned tag, float *d
 // read in one sweep, so for a small request the observation has arrived when the
 // request is seen. Leaves (leave = 1) on a GO2PI_RES_LEAVE header or idle_ticks
 // of the 100 MHz wall clock without a request.
-template <int SCOPE>
+template <int SCOPE, int NP = RES_POLL>
 __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned last, u64 idle_ticks, float *obsv,
                                              unsigned *err, int lane, int &leave, unsigned &e, int &B,
                                              unsigned &word) {
   u64 *qm = const_cast<u64 *>(q);
   const u64 t0 = wall_clock64();
-  const int npoll = min(1 + in_dim, 64 * RES_POLL);
+  const int npoll = min(1 + in_dim, 64 * NP);
   leave = 0;
   for (;;) {
-    u64 v[RES_POLL];
+    u64 v[NP];
 #pragma unroll
-    for (int u = 0; u < RES_POLL; ++u)
+    for (int u = 0; u < NP; ++u)
       if (u * 64 < npoll) v[u] = __hip_atomic_load(qm + min(u * 64 + lane, npoll - 1), __ATOMIC_RELAXED, SCOPE);
     const u64 h = __shfl(v[0], 0);
     const unsigned tag = (unsigned)(h >> 32);
@@ -113,7 +113,7 @@ __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned 
       if (1 + n <= npoll) {
         bool ok = true;
 #pragma unroll
-        for (int u = 0; u < RES_POLL; ++u) {
+        for (int u = 0; u < NP; ++u) {
           const int i = u * 64 + lane;
           if (u * 64 < npoll && i >= 1 && i <= n) {
             ok &= (unsigned)(v[u] >> 32) == e;
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   const int ks0 = ((RES_WAVES * 64) % P.L[0].N_pad == 0 && P.L[0].N_pad < RES_WAVES * 64) ? (RES_WAVES * 64) / P.L[0].N_pad : 0;
   float *cbase = p0 + (ks0 * GO2PI_SMALL_MAXB * P.L[0].N_pad + 3) / 4 * 4;
   const CtlLds CL = ctl_lds(cbase, GO2PI_SMALL_MAXB, P.in_dim);
+  float *craw = cbase + ctl_lds_floats(GO2PI_SMALL_MAXB, P.in_dim);  // CTL: [B][GO2PI_CTL_RAW + in_dim] request rows
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
@@ -274,9 +275,13 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       int leave = 0, B = 0;
       unsigned e = 0, word = 0;
       if (g == 0) {
-        // CTL: the header alone (the rows are plain floats in the staging)
-        wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, CTL ? 0 : in_dim, last, idle_ticks, obsv, err, lane, leave, e, B,
-                                                word);
+        // CTL: the header with the tick's rows as tagged granules (3 per lane per poll:
+        // one robot's 53 + in_dim floats arrive with the request); act: the observation
+        if constexpr (CTL)
+          wait_request<__HIP_MEMORY_SCOPE_SYSTEM, 3>(req, GO2PI_CTL_RAW + in_dim, last, idle_ticks, craw, err, lane,
+                                                     leave, e, B, word);
+        else
+          wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word);
         const int n = (leave || CTL) ? 0 : B * in_dim;
         for (int i = lane; i < n; i += 64)
           __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
@@ -304,17 +309,14 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     CtlView cv{};
     if constexpr (CTL) {
       if (g == 0) {
-        // the tick's raw rows from host memory (system scope: fresh every request)
+        // the request's rows (craw: state | joystick | previous obs | previous action, each
+        // B rows) into the assembly's LDS image
         const bool joy = (word & GO2PI_RES_JOY) != 0u;
-        auto fetch = [&](float *dst, const float *src, int cnt) {
-          for (int i = tid; i < cnt; i += RES_WAVES * 64)
-            dst[i] = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned *>(const_cast<float *>(src)) + i,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        };
-        fetch(CL.st, C.state, B * GO2PI_CTL_STATE_DIM);
-        if (joy) fetch(CL.jy, C.joy, B * GO2PI_CTL_JOY_DIM);
-        fetch(CL.act, C.action, B * GO2PI_CTL_DOF);
-        fetch(CL.obs, C.obs, B * in_dim);
+        const int o_jy = B * GO2PI_CTL_STATE_DIM, o_obs = o_jy + B * GO2PI_CTL_JOY_DIM, o_act = o_obs + B * in_dim;
+        for (int i = tid; i < o_jy; i += RES_WAVES * 64) CL.st[i] = craw[i];
+        for (int i = tid; i < B * GO2PI_CTL_JOY_DIM; i += RES_WAVES * 64) CL.jy[i] = craw[o_jy + i];
+        for (int i = tid; i < B * in_dim; i += RES_WAVES * 64) CL.obs[i] = craw[o_obs + i];
+        for (int i = tid; i < B * GO2PI_CTL_DOF; i += RES_WAVES * 64) CL.act[i] = craw[o_act + i];
         if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
         if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
         __syncthreads();
@@ -466,7 +468,10 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   const size_t ctl_off = ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
                           (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * p.L[0].K_pad +
                           (size_t)(KS > 1 ? KS : 0) * GO2PI_SMALL_MAXB * N0 + 3) / 4 * 4;
-  const size_t lds = sizeof(float) * (ctl_off + (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) : 0));
+  const size_t lds =
+      sizeof(float) * (ctl_off + (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) +
+                                            (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim)
+                                      : 0));
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
