@@ -62,11 +62,12 @@ typedef struct go2pi_opts {
   float action_clip;     /* > 0: clamp action to [-action_clip, action_clip]
                             (the caller's kActionLimit clamp, controller.cpp:217-223) */
   float action_scale;    /* != 0 and != 1: action <- action * action_scale (after clip) */
-  /* > 0: go2pi_run at batch <= 8 is served by a RESIDENT kernel (no launch per call:
-     the request and the observation travel as tagged granules in host-mapped memory);
-     the kernel leaves after this many ms without a request and is relaunched by the
-     next call. 0 (default): one launch per call. Any other call on the engine first
-     stops the resident kernel. */
+  /* > 0: go2pi_run and go2pi_controller_step at batch <= 8 are served by a RESIDENT
+     kernel (no launch per call: the request and its input rows travel as tagged
+     granules in host-mapped memory); the kernel leaves after this many ms without a
+     request and is relaunched by the next call. Dense (non-recurrent) policies whose
+     final layer is <= 16 wide; others keep the launch path. 0 (default): one launch
+     per call. Any other call on the engine first stops the resident kernel. */
   int32_t resident_ms;
 } go2pi_opts;
 
