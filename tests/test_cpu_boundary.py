@@ -152,18 +152,24 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu ", sizeof(go2pi_opts), offsetof(go2pi_opts, obs_mean),
          offsetof(go2pi_opts, action_scale), sizeof(go2pi_cost), offsetof(go2pi_cost, n_layers),
          offsetof(go2pi_opts, small_batch));
-  printf("%zu %zu %zu %zu\n", sizeof(go2pi_ctl_params), offsetof(go2pi_ctl_params, gravity_w),
+  printf("%zu %zu %zu %zu ", sizeof(go2pi_ctl_params), offsetof(go2pi_ctl_params, gravity_w),
          offsetof(go2pi_ctl_params, action_scale), offsetof(go2pi_ctl_params, q0));
+  go2pi_opts o;
+  go2pi_default_opts(&o);
+  printf("%zu %d\n", offsetof(go2pi_opts, resident_ms), o.resident_ms);
   return 0;
 }'''
     exe = os.path.join(ROOT, "build", "abi_layout")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
-    subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe], input=src, text=True,
-                   check=True)
+    lib = os.path.join(ROOT, "go2_onnx_controller_amd", "lib")
+    subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe, "-L", lib, "-lgo2pi",
+                    f"-Wl,-rpath,{lib}"], input=src, text=True, check=True)
     got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    # the resident kernel is opt-in: go2pi_default_opts leaves resident_ms at 0
     assert got == [ctypes.sizeof(Opts), Opts.obs_mean.offset, Opts.action_scale.offset, ctypes.sizeof(Cost),
                    Cost.n_layers.offset, Opts.small_batch.offset, ctypes.sizeof(CtlParams),
-                   CtlParams.gravity_w.offset, CtlParams.action_scale.offset, CtlParams.q0.offset]
+                   CtlParams.gravity_w.offset, CtlParams.action_scale.offset, CtlParams.q0.offset,
+                   Opts.resident_ms.offset, 0]
 
 
 def build_controller_shape():
