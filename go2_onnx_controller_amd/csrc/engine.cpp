@@ -52,6 +52,51 @@ struct ApiError : std::runtime_error {
 inline int ceil16(int x) { return (x + 15) & ~15; }
 inline int ceil64(int x) { return (x + 63) & ~63; }
 
+// Pinned host-mapped blocks are never returned to HIP while the process runs:
+// hipHostFree (like hipFree) performs an implicit hipDeviceSynchronize, which
+// waits for every live resident kernel of every other engine on the device (and
+// never returns while another thread keeps one of them busy). A destroyed
+// engine's blocks go to this process-wide cache and the next engine reuses them.
+std::mutex g_pin_mu;
+std::vector<std::pair<size_t, void *>> g_pin_free;  // (bytes, block)
+
+void *pin_take(size_t bytes) {
+  bytes = (bytes + 4095) & ~(size_t)4095;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    size_t best = g_pin_free.size();
+    for (size_t i = 0; i < g_pin_free.size(); ++i)
+      if (g_pin_free[i].first >= bytes && (best == g_pin_free.size() || g_pin_free[i].first < g_pin_free[best].first))
+        best = i;
+    if (best < g_pin_free.size()) {
+      void *p = g_pin_free[best].second;
+      g_pin_free.erase(g_pin_free.begin() + (long)best);
+      return p;
+    }
+  }
+  void *p = nullptr;
+  hip_check(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  return p;
+}
+
+void pin_give(void *p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_free.emplace_back((bytes + 4095) & ~(size_t)4095, p);
+}
+
+// Every entry point leaves the calling thread's current HIP device as it found it
+// (the engine switches to its own device for its work).
+struct DeviceRestore {
+  int prev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceRestore() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 }  // namespace
 
 struct go2pi_engine {
@@ -63,6 +108,7 @@ struct go2pi_engine {
   hipStream_t stream = nullptr;
   go2pi::DevProgram prog{};
   std::vector<void *> allocs;  // device allocations
+  std::vector<std::pair<size_t, void *>> pinned;  // pinned host blocks (returned to the cache)
   float *d_hidden = nullptr;   // [max_batch][H]
   float *d_obs = nullptr;      // host-path staging [max_batch][in]
   float *d_act = nullptr;      // [max_batch][out]
@@ -98,7 +144,12 @@ struct go2pi_engine {
   char *h_ctl = nullptr, *m_ctl = nullptr; // host path, batch <= SMALL_MAXB: pinned host-mapped staging
   char *d_ctlbuf = nullptr;                // host path, larger batches: device staging (lazy)
 
+  // Teardown touches only this engine's stream: no hipFree / hipHostFree /
+  // hipDeviceSynchronize, each of which would wait for every other engine's live
+  // resident kernel on the device (device memory is stream-ordered, pinned
+  // blocks go back to the process-wide cache).
   ~go2pi_engine() {
+    DeviceRestore keep;
     (void)hipSetDevice(device);
     if (resident_live) {  // tell the resident kernel to leave (the sync below waits for it)
       __atomic_store_n(h_req, (unsigned long long)GO2PI_RES_LEAVE << 32, __ATOMIC_SEQ_CST);
@@ -109,21 +160,32 @@ struct go2pi_engine {
       if (graphs[i]) (void)hipGraphExecDestroy(graphs[i]);
       if (graph_defs[i]) (void)hipGraphDestroy(graph_defs[i]);
     }
-    for (void *p : allocs) (void)hipFree(p);
-    if (h_obs) (void)hipHostFree(h_obs);
-    if (h_act) (void)hipHostFree(h_act);
-    if (h_err) (void)hipHostFree(h_err);
-    if (h_ctl) (void)hipHostFree(h_ctl);
-    if (h_req) (void)hipHostFree(h_req);
-    if (stream) (void)hipStreamDestroy(stream);
+    for (void *p : allocs) (void)hipFreeAsync(p, stream);
+    for (auto &b : pinned) pin_give(b.second, b.first);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
   }
 
+  // device memory: stream-ordered on the engine's stream (usable by any stream once
+  // dalloc returns)
   template <class T>
   T *dalloc(size_t count) {
     void *p = nullptr;
-    hip_check(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
+    hip_check(hipMallocAsync(&p, std::max<size_t>(count, 1) * sizeof(T), stream), "hipMallocAsync");
     allocs.push_back(p);
+    hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     return static_cast<T *>(p);
+  }
+  // pinned, host-mapped (fine-grained) memory and its device alias
+  template <class T>
+  void palloc(T **host, T **dev, size_t bytes) {
+    void *p = pin_take(bytes);
+    pinned.emplace_back(bytes, p);
+    std::memset(p, 0, bytes);
+    *host = static_cast<T *>(p);
+    if (dev) hip_check(hipHostGetDevicePointer((void **)dev, p, 0), "hipHostGetDevicePointer");
   }
   template <class T>
   T *upload(const std::vector<T> &v) {
@@ -196,7 +258,7 @@ struct go2pi_engine {
   void resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
     if (resident_live && resident_ctl != (ctl != nullptr)) resident_stop();  // the other form is live
     const int n = (int)batch * (model.in_dim + (ctl ? GO2PI_CTL_RAW : 0));
-    const auto idle = std::chrono::milliseconds(opts.resident_ms);
+    const auto idle = std::chrono::microseconds(1000LL * opts.resident_ms);  // (us: idle / 2 stays > 0 at 1 ms)
     for (int attempt = 0;; ++attempt) {
       // layer tags e + 1 + l: an epoch spans nl + 2 tags
       const unsigned span = (unsigned)prog.nl + 2;
@@ -226,10 +288,16 @@ struct go2pi_engine {
       }
       res_last = std::chrono::steady_clock::now();
       if (d == e0) return;
-      // the kernel left (idle exit racing this request, or a hand-off timeout): wait for
-      // it to drain, then serve the request from a fresh launch with a fresh epoch
+      // the kernel left: wait for it to drain. An idle exit racing this request is
+      // benign (serve it from a fresh launch with a fresh epoch); a hand-off timeout
+      // (h_err set) is a device-side protocol fault and is reported, not retried
       resident_stop();
-      __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
+      if (__atomic_load_n(h_err, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
+        throw HipError("resident kernel: a layer hand-off timed out (request not served)", GO2PI_E_DEVICE);
+      }
+      if (d != GO2PI_RES_LEAVE)
+        throw HipError("resident kernel did not answer within 2 s (request not served)", GO2PI_E_DEVICE);
       if (attempt >= 1) throw HipError("resident kernel did not serve the request", GO2PI_E_DEVICE);
     }
   }
@@ -441,7 +509,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     flops += 2.0 * 3 * H * ((double)m.gru.I + H);
     wbytes += 4.0 * (3.0 * H * (m.gru.I + H) + 6.0 * H);
     e.d_hidden = e.dalloc<float>((size_t)e.opts.max_batch * H);
-    hip_check(hipMemset(e.d_hidden, 0, (size_t)e.opts.max_batch * H * sizeof(float)), "hipMemset");
+    hip_check(hipMemsetAsync(e.d_hidden, 0, (size_t)e.opts.max_batch * H * sizeof(float), e.stream), "hipMemsetAsync");
   } else {
     p.in_pad = p.L[0].K_pad;
   }
@@ -515,14 +583,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.tmp_stride = maxw;
   e.d_tmp[0] = e.dalloc<float>((size_t)GO2PI_SMALL_MAXB * maxw);
   e.d_tmp[1] = e.dalloc<float>((size_t)GO2PI_SMALL_MAXB * maxw);
-  hip_check(hipHostMalloc((void **)&e.h_obs, sizeof(float) * GO2PI_SMALL_MAXB * m.in_dim,
-                          hipHostMallocMapped | hipHostMallocCoherent),
-            "hipHostMalloc");
-  hip_check(hipHostMalloc((void **)&e.h_act, sizeof(float) * GO2PI_SMALL_MAXB * m.out_dim,
-                          hipHostMallocMapped | hipHostMallocCoherent),
-            "hipHostMalloc");
-  hip_check(hipHostGetDevicePointer((void **)&e.m_obs, e.h_obs, 0), "hipHostGetDevicePointer");
-  hip_check(hipHostGetDevicePointer((void **)&e.m_act, e.h_act, 0), "hipHostGetDevicePointer");
+  e.palloc(&e.h_obs, &e.m_obs, sizeof(float) * GO2PI_SMALL_MAXB * m.in_dim);
+  e.palloc(&e.h_act, &e.m_act, sizeof(float) * GO2PI_SMALL_MAXB * m.out_dim);
 
   // single-launch small-batch path: dense programs whose layers fit the kernel's
   // register slots (K_pad <= 1024) and whose widest layer fits one resident grid
@@ -531,15 +593,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     for (int l = 0; l < p.nl; ++l) kmax = std::max(kmax, p.L[l].K_pad);
     e.latency_ok = !m.has_gru && kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
                    !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
-    hip_check(hipHostMalloc((void **)&e.h_err, 512, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
-    std::memset(e.h_err, 0, 512);
-    hip_check(hipHostGetDevicePointer((void **)&e.m_err, e.h_err, 0), "hipHostGetDevicePointer");
+    e.palloc(&e.h_err, &e.m_err, 512);
     p.err = e.m_err + 64;  // batched kernel hand-off timeouts
     if (e.latency_ok) {
       e.gstride = GO2PI_SMALL_MAXB * maxw;
       const size_t ng = (size_t)std::max(1, p.nl - 1) * e.gstride;
       e.d_gran = e.dalloc<unsigned long long>(ng);
-      hip_check(hipMemset(e.d_gran, 0, ng * sizeof(unsigned long long)), "hipMemset");
+      hip_check(hipMemsetAsync(e.d_gran, 0, ng * sizeof(unsigned long long), e.stream), "hipMemsetAsync");
       e.h_done = e.h_err + 32;  // 128 B apart: its own cache line
       e.m_done = e.m_err + 32;
       e.done_ok = p.L[p.nl - 1].N_pad == 16;
@@ -548,11 +608,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     if (e.latency_ok && e.done_ok && e.opts.resident_ms > 0) {
       // room for a controller tick's rows too (GO2PI_CTL_RAW + in_dim floats per robot)
       const size_t nreq = 1 + GO2PI_SMALL_MAXB * (size_t)(m.in_dim + GO2PI_CTL_RAW);
-      hip_check(hipHostMalloc((void **)&e.h_req, sizeof(unsigned long long) * nreq,
-                              hipHostMallocMapped | hipHostMallocCoherent),
-                "hipHostMalloc");
-      std::memset(e.h_req, 0, sizeof(unsigned long long) * nreq);
-      hip_check(hipHostGetDevicePointer((void **)&e.m_req, e.h_req, 0), "hipHostGetDevicePointer");
+      e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
       e.d_mirror = e.dalloc<unsigned long long>(1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim);
       int khz = 0;
       hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.device), "hipDeviceGetAttribute");
@@ -564,12 +620,12 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   if (std::getenv("GO2PI_DIAG_STAMPS")) {  // diagnostics: per-workgroup clock stamps
     e.n_stamps = GO2PI_STAMPS_PER_WG * ((e.opts.max_batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
     p.stamps = e.dalloc<unsigned long long>(e.n_stamps);
-    hip_check(hipMemset(p.stamps, 0, e.n_stamps * sizeof(unsigned long long)), "hipMemset");
+    hip_check(hipMemsetAsync(p.stamps, 0, e.n_stamps * sizeof(unsigned long long), e.stream), "hipMemsetAsync");
   }
   // the finished program, copied to device memory for the latency kernel
   {
     float *z = e.dalloc<float>(64);
-    hip_check(hipMemset(z, 0, 64 * sizeof(float)), "hipMemset");
+    hip_check(hipMemsetAsync(z, 0, 64 * sizeof(float), e.stream), "hipMemsetAsync");
     p.zero = z;
   }
   // controller tick: a policy with kHistory x 49 observations and 12 actions
@@ -583,7 +639,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   }
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
-  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  // (not hipDeviceSynchronize: that would wait for other engines' resident kernels)
+  hip_check(hipStreamSynchronize(e.stream), "hipStreamSynchronize");
+  hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
 
   e.cost.flops_per_row = flops;
   e.cost.weight_bytes = wbytes;
@@ -592,8 +650,11 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.cost.has_gru = p.has_gru;
 }
 
+// Every C-ABI entry point runs through here: exceptions become status codes, and
+// the caller's current HIP device is restored on the way out.
 template <class F>
 int guarded(F &&f) {
+  DeviceRestore keep;
   try {
     g_last_error.clear();
     return f();
@@ -945,9 +1006,7 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
     char *dev;  // device-side view of the staging
     if (small) {
       if (!e->h_ctl) {
-        hip_check(hipHostMalloc((void **)&e->h_ctl, L.total, hipHostMallocMapped | hipHostMallocCoherent),
-                  "hipHostMalloc");
-        hip_check(hipHostGetDevicePointer((void **)&e->m_ctl, e->h_ctl, 0), "hipHostGetDevicePointer");
+        e->palloc(&e->h_ctl, &e->m_ctl, L.total);
       }
       std::memcpy(e->h_ctl + L.state, state, n_state);
       if (joy) std::memcpy(e->h_ctl + L.joy, joy, n_joy);
@@ -1033,6 +1092,9 @@ int go2pi_controller_step_device(go2pi_engine *e, const float *state, const floa
     if (batch == 0) return GO2PI_OK;
     if (!state || !obs || !action) throw ApiError("null state/obs/action buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
+    // a live resident kernel shares the granules, epoch and error words the batch <= 8
+    // launch uses: it leaves first (as for every other call on the engine)
+    e->resident_stop();
     go2pi::DevCtl c{e->d_ctl, state, joy, obs, action, q_des, kp, kd, status};
     e->enqueue_ctl(c, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;

@@ -454,16 +454,17 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, void *stream) {
   if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
-  int grid = 1;
-  for (int l = 0; l < p.nl; ++l) {
+  for (int l = 0; l < p.nl; ++l)
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
-    grid = std::max(grid, p.L[l].N_pad >> 4);
-  }
   // local layer 0 where each thread's share of it fits NF = 8 or 16 registers' fragments
   const int N0 = p.L[0].N_pad, C0 = p.L[0].K_pad >> 4;
   const int KS = (N0 > 0 && (RES_WAVES * 64) % N0 == 0) ? (RES_WAVES * 64) / N0 : 0;
   const int nf = (KS > 0 && C0 % KS == 0) ? 4 * (C0 / KS) : 0;
   const bool local0 = p.nl >= 2 && (nf == 8 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
+  // one workgroup per 16-output tile of the widest TILED layer (with a local layer 0,
+  // workgroups beyond the later layers' tiles would only repeat layer 0 and poll)
+  int grid = 1;
+  for (int l = local0 ? 1 : 0; l < p.nl; ++l) grid = std::max(grid, p.L[l].N_pad >> 4);
   // (the kernel's LDS carve-up: x0 and p0 are laid out whether used or not)
   const size_t ctl_off = ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
                           (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * p.L[0].K_pad +

@@ -249,3 +249,28 @@ int gruref_step_f64(int I, int H, const float *W, const float *R, const float *W
   }
   return 0;
 }
+
+/*
+ * cpu_baseline leg of bench.py (BASELINE configs[0]): the reference's own
+ * measurement is one timed act() at batch 1 (onnx_inference/src/cpp/main.cpp:38-42,
+ * steady_clock around Session::Run). This times `warm + iters` single-robot fp32
+ * forwards on the calling thread (no OpenMP), each bracketed by CLOCK_MONOTONIC,
+ * and writes the `iters` per-call durations in microseconds to out_us. Each call
+ * reads the observation row and writes the action row, as act() does.
+ */
+#include <time.h>
+int mlpref_time_b1(void *p, const float *x, float *y, int warm, int iters, double *out_us) {
+  const mlpref_t *h = (const mlpref_t *)p;
+  if (!h || iters < 0 || warm < 0) return -1;
+  float *a = (float *)malloc(sizeof(float) * RB * h->maxw);
+  float *bb = (float *)malloc(sizeof(float) * RB * h->maxw);
+  for (int i = 0; i < warm + iters; ++i) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    block_f32(h, x, y, 1, h->K[0], h->N[h->nl - 1], a, bb);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (i >= warm) out_us[i - warm] = (double)(t1.tv_sec - t0.tv_sec) * 1e6 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-3;
+  }
+  free(a); free(bb);
+  return 0;
+}

@@ -42,6 +42,7 @@ def lib():
         L.mlpref_run_f32.argtypes = [P, P, P, ctypes.c_long, ctypes.c_int]
         L.mlpref_run_f64.argtypes = [P, P, P, ctypes.c_long, ctypes.c_int]
         L.mlpref_destroy.argtypes = [P]
+        L.mlpref_time_b1.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, P]
         L.gruref_step_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, P, P,
                                       ctypes.c_long, ctypes.c_int]
         _lib = L
@@ -125,6 +126,16 @@ class MlpRef:
         y = np.empty((x.shape[0], self.out_dim), np.float64)
         lib().mlpref_run_f64(self._h, x.ctypes.data, y.ctypes.data, x.shape[0], nthreads)
         return y
+
+    def time_b1(self, x, warm=1000, iters=10000):
+        """Per-call microseconds of `iters` single-robot fp32 forwards of row x (after
+        `warm` untimed ones), timed inside C on the calling thread (bench.py cpu_baseline)."""
+        x = np.ascontiguousarray(x, np.float32).reshape(-1)[: self.in_dim]
+        y = np.empty(self.out_dim, np.float32)
+        out = np.empty(iters, np.float64)
+        if lib().mlpref_time_b1(self._h, x.ctypes.data, y.ctypes.data, int(warm), int(iters), out.ctypes.data):
+            raise RuntimeError("mlpref_time_b1 failed")
+        return out
 
     def __del__(self):
         try:

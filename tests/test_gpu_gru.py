@@ -125,3 +125,36 @@ def test_gru_inference_session_explicit_hidden(synth_path):
     want_y, want_h = _oracle_rollout(p, x, h0=h[0])
     assert abs_err(act, want_y[0]) <= TOL
     assert abs_err(h_out[0], want_h) <= TOL
+
+
+def test_gru256_sequence_100_ticks_b4096(synth_path):
+    """BASELINE configs[4] as specified: 4096 robots, T = 100 ticks through the
+    sequence path (go2pi_run_sequence_device: h0 = 0, hidden rows carried in LDS
+    between ticks), checked against the fp64 ONNX-GRU oracle on the actions of every
+    tick and on h at t = 100, on 256 sampled robots (rows are independent; the sample
+    covers the first and last 16-robot tiles). The per-tick device path over the same
+    100 ticks must be bitwise identical to the sequence."""
+    import torch
+    from go2_onnx_controller_amd import Engine
+    p = synth_path("go2_gru_256")
+    T, B = 100, 4096
+    g = torch.Generator().manual_seed(100)
+    x = torch.randn((T, B, 48), generator=g)
+    rng = np.random.default_rng(100)
+    rows = np.unique(np.concatenate([np.arange(16), np.arange(B - 16, B), rng.choice(B, 224, replace=False)]))
+    want_y, want_h = _oracle_rollout(p, x[:, rows].numpy())
+    xd = x.to("cuda:0")
+    with Engine(p, max_batch=B) as a, Engine(p, max_batch=B) as b:
+        a.reset_hidden()
+        ya = a.run_sequence_torch(xd)
+        torch.cuda.synchronize()
+        ha = a.get_hidden(B)
+        y = ya.cpu().numpy()
+        for t in range(T):
+            assert abs_err(y[t, rows], want_y[t]) <= TOL, f"tick {t}"
+        assert abs_err(ha[rows], want_h) <= TOL
+        b.reset_hidden()
+        yb = torch.stack([b.run_torch(xd[t].contiguous()) for t in range(T)])
+        torch.cuda.synchronize()
+        assert torch.equal(ya, yb)
+        np.testing.assert_array_equal(ha, b.get_hidden(B))

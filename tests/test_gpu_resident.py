@@ -14,7 +14,7 @@ import time
 import numpy as np
 import pytest
 
-from conftest import SHIPPED, abs_err, realistic_obs
+from conftest import SHIPPED, abs_err, realistic_obs, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -132,3 +132,109 @@ def test_resident_prologue_epilogue(synth_path):
         for B in (1, 2, 8, 1):
             x = rng.normal(0, 2, (B, 48)).astype(np.float32)
             assert abs_err(r.run(x), p.run(x)) <= TOL
+
+
+def test_create_destroy_while_other_engine_resident(synth_path):
+    """Engine B is created and destroyed while engine A's resident kernel is kept live
+    by another thread (a 200 Hz act() loop, faster than A's idle bound): neither
+    create nor destroy may wait on A's kernel (no device-wide synchronisation)."""
+    import threading
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    ref = mlp_ref.MlpRef.from_onnx(SHIPPED)
+    stop, errs = threading.Event(), []
+    with Engine(SHIPPED, max_batch=8, resident_ms=100) as a:
+        x = realistic_obs(1, seed=1)
+        a.run(x)
+
+        def tick():
+            try:
+                while not stop.is_set():
+                    if abs_err(a.run(x), ref.f64(x)) > TOL:
+                        errs.append("A's output changed")
+                    time.sleep(0.005)
+            except Exception as ex:  # noqa: BLE001 - reported below
+                errs.append(repr(ex))
+        th = threading.Thread(target=tick)
+        th.start()
+        try:
+            time.sleep(0.05)
+            path = synth_path("go2_mlp_512")
+            for _ in range(3):
+                t0 = time.perf_counter()
+                b = Engine(path, max_batch=64)
+                y = b.run(np.ones((2, 48), np.float32))
+                b.close()
+                dt = time.perf_counter() - t0
+                assert np.isfinite(y).all()
+                assert dt < 1.0, f"create + run + destroy took {dt:.2f} s beside a live resident kernel"
+        finally:
+            stop.set()
+            th.join(timeout=10)
+    assert not errs, errs
+
+
+def test_resident_controller_step_then_device_step():
+    """go2pi_controller_step (served by the resident kernel at B <= 8) alternating with
+    go2pi_controller_step_device on the same engine: the device call stops the resident
+    kernel first (they share granules and the epoch), both match the oracle."""
+    import torch
+    from go2_onnx_controller_amd import Engine
+    from oracle import controller_ref as cr
+    from oracle import mlp_ref
+    ref = mlp_ref.MlpRef.from_onnx(SHIPPED)
+    rng = np.random.default_rng(21)
+    dev = torch.device("cuda:0")
+    with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
+        for i in range(6):
+            B = 1 + i % 4
+            st, joy = cr.synthetic_states(rng, B), cr.synthetic_joy(rng, B)
+            obs = rng.standard_normal((B, 98)).astype(np.float32)
+            act = rng.standard_normal((B, 12)).astype(np.float32)
+            want_obs, _ = cr.assemble_obs(obs, act, st, joy, 2)
+            a_ref = cr.post_process(ref.f64(want_obs), joy)[0]
+            if i % 2 == 0:
+                e.controller_step(st, obs, act, joy=joy)
+                o, a = obs, act
+            else:
+                t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+                     for k, v in (("st", st), ("joy", joy), ("obs", obs), ("act", act))}
+                e.controller_step_torch(t["st"], t["obs"], t["act"], joy=t["joy"])
+                torch.cuda.synchronize(dev)
+                o, a = t["obs"].cpu().numpy(), t["act"].cpu().numpy()
+            assert np.array_equal(o, want_obs), f"tick {i}: observation differs"
+            assert rel_err(a, a_ref) <= TOL, f"tick {i}"
+
+
+def test_entry_points_restore_current_device():
+    """Every C-ABI call switches to the engine's device for its work and restores the
+    caller's current device (with one GPU this checks the ordinal is left alone; with
+    two or more, an engine on the last device is driven while the caller sits on 0)."""
+    import torch
+    from go2_onnx_controller_amd import Engine
+    from oracle import controller_ref as cr
+    n = torch.cuda.device_count()
+    edev = n - 1
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(4)
+    with Engine(SHIPPED, device=edev, max_batch=64, resident_ms=200) as e:
+        assert torch.cuda.current_device() == 0
+        x = realistic_obs(3)
+        e.run(x)
+        assert torch.cuda.current_device() == 0
+        e.run(realistic_obs(1))  # resident path
+        assert torch.cuda.current_device() == 0
+        d = torch.device(f"cuda:{edev}")
+        xo = torch.from_numpy(realistic_obs(64)).to(d)
+        with torch.cuda.device(d):
+            s = torch.cuda.Stream(d)
+        torch.cuda.set_device(0)
+        e.run_torch(xo, stream=s)
+        assert torch.cuda.current_device() == 0
+        st, joy = cr.synthetic_states(rng, 2), cr.synthetic_joy(rng, 2)
+        obs, act = np.zeros((2, 98), np.float32), np.zeros((2, 12), np.float32)
+        e.controller_step(st, obs, act, joy=joy)
+        assert torch.cuda.current_device() == 0
+        e.sync()
+        assert torch.cuda.current_device() == 0
+    assert torch.cuda.current_device() == 0
