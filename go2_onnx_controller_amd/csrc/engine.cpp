@@ -368,8 +368,8 @@ namespace {
 // K is padded to a multiple of 64 (4 chunks: the kernel's unroll); a hidden layer's
 // N to its consumer's K_pad (64), the final layer's N to 16 (one MFMA tile).
 void pack_dense(const go2pi::Dense &d, bool last, std::vector<float> &w, std::vector<float> &b, int &K_pad,
-                int &N_pad) {
-  K_pad = ceil64(d.K);
+                int &N_pad, int kq = 64) {
+  K_pad = kq == 16 ? ceil16(d.K) : ceil64(d.K);
   N_pad = last ? ceil16(d.N) : ceil64(d.N);
   const int T = N_pad / 16, C = K_pad / 16;
   w.assign((size_t)T * C * 64 * 4, 0.f);
@@ -423,6 +423,25 @@ void set_ctl_params(go2pi_engine &e, const go2pi_ctl_params &cp) {
   hip_check(hipMemcpy(e.d_ctl, &d, sizeof(d), hipMemcpyHostToDevice), "hipMemcpy");
 }
 
+// The 4-wave uniform-MLP pipeline (fused_impl.hpp w4_step) applies to a policy
+// whose hidden layers are all 64 * TPW wide (TPW = 2, 4 or 8) with one
+// activation, and whose final layer is at most 2 tiles wide (1 at TPW = 8); a GRU
+// in front needs H % 64 == 0. It is the default (waves = 0) wherever it applies:
+// measured faster than the generic 8-wave body.
+bool w4_eligible(const go2pi_engine &e, const go2pi::Model &m) {
+  const int nl = (int)m.layers.size();
+  if (!(e.opts.waves == 0 || e.opts.waves == 4) || nl < 2) return false;
+  if (m.has_gru && m.gru.H % 64) return false;
+  if (std::getenv("GO2PI_NO_HEAD_FUSE") || std::getenv("GO2PI_NO_W4")) return false;  // env: A/B diagnostics only
+  const int tpw = ceil64(m.layers[0].N) / 64, t_last = ceil16(m.layers[nl - 1].N) / 16;
+  if (!(tpw == 2 || tpw == 4 || tpw == 8) || t_last > (tpw == 8 ? 1 : 2)) return false;
+  for (int l = 0; l + 1 < nl; ++l)
+    if (ceil64(m.layers[l].N) != 64 * tpw || m.layers[l].act != m.layers[0].act ||
+        m.layers[l].alpha != m.layers[0].alpha)
+      return false;
+  return true;
+}
+
 void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o) {
   go2pi_default_opts(&e.opts);
   if (o) {
@@ -468,12 +487,24 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   p.out_dim = m.out_dim;
   int maxw = 0;
   double flops = 0, wbytes = 0;
+  // The 4-wave pipeline (decided below) takes a layer 0 of 3 (mod 4) k-chunks:
+  // a 48- or 98-wide observation is padded to 16 columns, not 64 (25 % / 12.5 %
+  // fewer layer-0 MFMAs and fragment bytes). Other kernels take any chunk count.
+  const bool w4_shape = w4_eligible(e, m);
+  const int k0q = (w4_shape && !m.has_gru && (ceil16(m.layers[0].K) / 16) % 4 == 3 && !std::getenv("GO2PI_K0_PAD64"))
+                      ? 16 : 64;  // env: A/B diagnostics only
+  // every dense layer's fragments back to back in one arena (the pipeline finds
+  // layer l from the base: fused_impl.hpp w4_layer_w)
+  std::vector<std::vector<float>> packed(p.nl);
+  size_t arena = 0;
+  std::vector<size_t> off(p.nl);
   for (int l = 0; l < p.nl; ++l) {
-    std::vector<float> w, b;
+    std::vector<float> b;
     int kp, np;
-    pack_dense(m.layers[l], l == p.nl - 1, w, b, kp, np);
+    pack_dense(m.layers[l], l == p.nl - 1, packed[l], b, kp, np, l == 0 ? k0q : 64);
+    off[l] = arena;
+    arena += packed[l].size();
     auto &L = p.L[l];
-    L.w = e.upload(w);
     L.bias = e.upload(b);
     L.K_pad = kp;
     L.N_pad = np;
@@ -483,6 +514,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     maxw = std::max({maxw, kp, np});
     flops += 2.0 * m.layers[l].K * m.layers[l].N;
     wbytes += 4.0 * ((double)m.layers[l].K * m.layers[l].N + m.layers[l].N);
+  }
+  {
+    std::vector<float> all;
+    all.reserve(arena);
+    for (auto &v : packed) all.insert(all.end(), v.begin(), v.end());
+    const float *base = e.upload(all);
+    for (int l = 0; l < p.nl; ++l) p.L[l].w = base + off[l];
   }
   if (m.has_gru) {
     std::vector<float> w;
@@ -529,13 +567,10 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   // default (waves = 0) wherever it applies: measured faster than the generic
   // 8-wave body; otherwise waves = 0 means 8.
   // (a GRU policy runs its cell first and hands h' to the pipeline as layer 0's input)
-  if ((e.opts.waves == 0 || e.opts.waves == 4) && p.nl >= 2 && (!m.has_gru || m.gru.H % 64 == 0) &&
-      !std::getenv("GO2PI_NO_HEAD_FUSE") && !std::getenv("GO2PI_NO_W4")) {  // env: A/B diagnostics only
+  if (w4_shape) {
     const int t_last = p.L[p.nl - 1].N_pad / 16;
     const int tpw = p.L[0].N_pad / 64;
-    bool uniform = (tpw == 2 || tpw == 4 || tpw == 8) && t_last <= (tpw == 8 ? 1 : 2);
-    for (int l = 0; l + 1 < p.nl; ++l) uniform = uniform && p.L[l].N_pad == 64 * tpw;
-    if (uniform) {
+    {
       e.waves = 4;
       p.head_fuse = t_last;
       p.w4_tpw = tpw;
@@ -575,7 +610,6 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   if (lds > 160 * 1024)
     throw ApiError("layer width " + std::to_string(maxw) + " needs " + std::to_string(lds) +
                    " B of LDS per tile (> 160 KiB)", GO2PI_E_MODEL);
-  hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
 
   // buffers
   e.d_obs = e.dalloc<float>((size_t)e.opts.max_batch * m.in_dim);
@@ -637,6 +671,31 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     go2pi_ctl_default_params(&cp);
     set_ctl_params(e, cp);
   }
+  // the pipeline's hot block (program.hpp): what it reads, in one scalar burst
+  if (p.w4_tpw) {
+    const auto &H = p.L[p.nl - 1];
+    p.l0_w = p.L[0].w;
+    p.head_w = H.w;
+    p.head_bias = H.bias;
+    p.bpack = p.w4_bpack;
+    p.zero_hot = p.zero;
+    p.err_hot = p.err;
+    p.nbias = p.w4_bias;
+    p.head_n = H.N;
+    p.c0 = p.L[0].K_pad / 16;
+    p.in_dim_hot = p.in_dim;
+    p.hid_act = p.L[0].act;
+    p.hid_alpha = p.L[0].alpha;
+    p.head_act = H.act;
+    p.head_alpha = H.alpha;
+    p.w4_c0m = p.c0 % 4;
+    // the lean kernel: no prologue / epilogue arithmetic, no recurrent cell, and an
+    // LDS row no wider than the hidden layers
+    p.w4_plain = !p.has_gru && !p.pre_sub && !p.pre_div && !(p.obs_clip > 0.f) && !p.post_tanh &&
+                 std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) && p.clip_hi > 0 &&
+                 p.scale == 1.f && p.lds_stride == 64 * p.w4_tpw + 4 && !std::getenv("GO2PI_NO_PLAIN");
+  }
+  hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
   // (not hipDeviceSynchronize: that would wait for other engines' resident kernels)
@@ -1125,7 +1184,11 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     check_engine(e);
     if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
     const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
-    std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d>", e->waves, t, h);
+    const int c0m = t ? e->prog.w4_c0m : 0;
+    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4>
+      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d>", t, h, c0m);
+    else
+      std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d>", e->waves, t, h, c0m);
     return GO2PI_OK;
   });
 }

@@ -25,1562 +25,9 @@
 // 1e-5 fp32 vs the CPU path), while every robot row is computed with an
 // identical instruction sequence wherever it sits in the batch: sharded and
 // unsharded runs are bit-identical.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <type_traits>
-
-#include "ctl_fn.hpp"
-#include "device_fn.hpp"
-#include "program.hpp"
+#include "fused_impl.hpp"
 
 namespace go2pi {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-#if defined(GO2PI_DIAG_RD2)
-#define GO2PI_RING_RD 2
-#elif defined(GO2PI_DIAG_RD3)
-#define GO2PI_RING_RD 3
-#else
-#define GO2PI_RING_RD 1  // chunks ahead of the weight-fragment ring at 4 waves per workgroup (2, 3: slower)
-#endif
-// the 4-wave pipeline's ring depth by tiles per wave: a chunk is 4 * TPW MFMAs
-// (32 cycles each), and a fragment must be issued >= ~1K cycles (an L2 round trip
-// under load) before its MFMA
-#ifndef GO2PI_DIAG_RD2
-#ifndef GO2PI_DIAG_RD3
-#define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? 1 : ((TPW) >= 4 ? 2 : 3))
-#endif
-#endif
-#ifndef GO2PI_W4_RD
-#define GO2PI_W4_RD(TPW) GO2PI_RING_RD
-#endif
-#ifndef GO2PI_WPOL  // weight-fragment load policy: 0 plain, 1 nt, 2 sc1 (L1 bypass)
-#if defined(GO2PI_DIAG_NT)
-#define GO2PI_WPOL 1
-#elif defined(GO2PI_DIAG_SC1)
-#define GO2PI_WPOL 2
-#else
-#define GO2PI_WPOL 0
-#endif
-#endif
-#define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
-
-// Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
-//   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
-//   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-#ifdef GO2PI_DIAG_NOMFMA
-  c.x = fmaf(a, b, c.x);
-  return c;
-#else
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// Dense contraction over k-chunks [c0, c1) for TPW consecutive 16-col tiles.
-// X: LDS activations [16][xs], W: this layer's fragments (chunk-major: the
-// float4 stride between consecutive chunks of one tile is TL * 64).
-
-// component j of a float4 (j a compile-time constant after unrolling)
-__device__ __forceinline__ float f4c(const float4 &v, int j) {
-  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
-}
-
-// one weight fragment (GO2PI_DIAG_NOLOAD: register arithmetic instead, diagnostics)
-__device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int i) {
-#ifdef GO2PI_DIAG_NOLOAD
-  const float v = __int_as_float(0x3c000000 ^ ((c * 7 + i) & 0xff));
-  (void)p;
-  (void)cs;
-  return make_float4(v, v, v, v);
-#elif GO2PI_WPOL == 1
-  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p + c * cs));
-  return make_float4(v.x, v.y, v.z, v.w);
-#else
-  return p[c * cs];
-#endif
-}
-
-// Weight-fragment stream over a buffer resource: one SGPR descriptor per layer,
-// a per-lane byte offset per tile and the chunk offset folded into the scalar
-// offset. GO2PI_WPOL == 2 sets sc1 on the loads (served by the XCD's L2,
-// bypassing the CU's 32 KiB L1, which the fragments in flight would overrun).
-struct WStream {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ explicit WStream(const void *base)
-      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000)) {}
-  __device__ __forceinline__ float4 ld(int voff, int soff) const {
-#ifdef GO2PI_DIAG_NOLOAD
-    const float v = __int_as_float(0x3c000000 ^ ((voff + soff) & 0xff));
-    return make_float4(v, v, v, v);
-#else
-    constexpr int AUX = GO2PI_WPOL == 2 ? 16 : (GO2PI_WPOL == 1 ? 2 : 0);
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
-#endif
-  }
-};
-
-// Schedule (measured on MI355X with tools/clock_probe.py, cycles per 16-robot
-// workgroup of the 48->512^3->12 step): every tile's fragment for chunk c+1 is
-// loaded right after that tile's 4 MFMAs of chunk c, so each wave keeps exactly
-// one chunk in flight and its load issue is spread between MFMAs. Alternatives
-// measured slower: no prefetch 110K (8 waves: 113K), one chunk ahead issued as a
-// burst 123K/145K, three ahead 128K/144K, vs 104K-106K for this one; the
-// MFMA-only ablation (no weight loads) is 97K-99K. sched_barrier(0) pins the
-// order (hipcc otherwise sinks loads next to their uses). Tiles beyond T clamp
-// to T - 1 (duplicate loads, results unused); loads past c1 clamp to c1 - 1.
-// Requires (c1 - c0) % 4 == 0 (K padded to 64).
-//
-// Hand-off between two wide layers without a workgroup barrier (Handoff):
-// wave w publishes flags[w] = ep once its tiles of a layer are stored in LDS;
-// a wave of the next layer starts on the 4-chunk group that its own tiles form
-// (rotated chunk order, g0) and, before reading any group's A operands, waits
-// until that group's producer waves have published ep. A wave therefore reads
-// a group only after its producers stored it (RAW), and every producer sets
-// its flag only after its own contraction of the layer before, which read the
-// buffer this layer's epilogue overwrites (ping-pong WAR): by the end of its
-// contraction a consumer has seen every producer's flag. The rotation changes
-// the summation order of K chunks per wave, identically for every robot row.
-struct Handoff {
-  const int *flags;  // LDS, one int per wave; nullptr: the input is complete (barrier before)
-  int ep;            // epoch every producer of the input must have published
-  int tpw;           // producer tiles per wave
-  // cross-layer prefetch (barrier hand-off only): this wave's first tile
-  // group's chunk-0 fragments, loaded before the barrier (prefetch_first)
-  float4 pre[4];
-  int npre;       // valid entries of pre (0: none)
-  unsigned *err;  // set to 1 when a poll runs out of its bound (the engine raises it)
-};
-
-// Issue this wave's first weight fragments of layer L (chunk 0 of its first
-// tile group) before the barrier that completes L's input: they do not depend
-// on the activations, and the barrier waits on LDS only (lgkmcnt), so the
-// loads stay in flight across it. Same addresses as dense_acc's first loads.
-template <int NW>
-__device__ __forceinline__ void prefetch_first(const DevLayer &L, int wave, int lane, Handoff &h) {
-  const int T = L.N_pad >> 4;
-  if (T < NW) return;  // narrow layer: split-K path, no tile groups
-  constexpr int NP = NW >= 16 ? 2 : 4;  // min(G, 4)
-  const int t = wave * ((T + NW - 1) / NW);
-  const float4 *W = reinterpret_cast<const float4 *>(L.w);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) h.pre[i] = load_frag(W + (size_t)min(t + i, T - 1) * 64 + lane, 0, 0, i);
-  h.npre = NP;
-}
-
-__device__ __forceinline__ void handoff_wait(const Handoff &h, int c, int nw, int lane, bool &all) {
-  if (!h.flags || all) return;
-  const int wlo = c / h.tpw, whi = (c + 3) / h.tpw;  // producers of chunks c..c+3 (= tiles)
-  const unsigned long long need = ((2ull << whi) - 1) & ~((1ull << wlo) - 1);
-  for (int it = 0; it < (1 << 20); ++it) {  // bounded: ~30 ms, a protocol bug must not hang the GPU
-    const int f =
-        lane < nw ? __hip_atomic_load(h.flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : h.ep;
-    const unsigned long long ok = __ballot(f >= h.ep);
-    if (ok == ~0ull) {
-      all = true;  // every producer is done: no further polls this layer
-      break;
-    }
-    if ((ok & need) == need) break;
-    if (it == (1 << 20) - 1 && lane == 0 && h.err)  // never silently: outputs of this launch are invalid
-      __hip_atomic_store(h.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");  // the group's A-operand reads stay after the poll
-}
-
-__device__ __forceinline__ void handoff_publish(int *flags, int wave, int lane, int ep) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
-  if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int TPW>
-__device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *__restrict__ W, int TL, int t_first,
-                                          int T, int c0, int c1, int lane, f32x4 (&acc)[TPW],
-                                          const Handoff &h = Handoff{nullptr, 0, 1}, int g0 = 0, int nw = 0) {
-  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  const WStream ws(W);
-  int vo[TPW];                // per-lane byte offset of each tile's fragment in chunk 0
-  const int csb = TL * 1024;  // bytes per chunk (all tiles)
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) vo[i] = (min(t_first + i, T - 1) * 64 + lane) * 16;
-  if (c0 >= c1) return;
-  const int NG = (c1 - c0) >> 2;
-  int g = g0 % NG;
-  float4 cur[TPW];
-  if (TPW <= 4 && !h.flags && h.npre >= TPW && c0 == 0) {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) cur[i] = h.pre[i < 4 ? i : 0];  // prefetched before the barrier
-  } else {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) cur[i] = ws.ld(vo[i], (c0 + 4 * g) * csb);
-  }
-  // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
-  // a trailing load would only be waited for by the epilogue
-  // (A operands are read per 4-chunk group; double-buffering them across groups
-  // measured slower: 100.4K vs 97.8K cycles per workgroup; fragments 2 chunks
-  // ahead instead of 1 measured slower too: 98.1K vs 96.2K)
-  auto group = [&](int c, int cnext, auto tail_k) {
-    constexpr bool TAIL = decltype(tail_k)::value;
-    float4 a[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int cn = u < 3 ? c + u + 1 : cnext;  // the next group's first chunk (rotated order)
-      const bool LOAD = !(TAIL && u == 3);  // folded after unrolling
-      float4 nxt[TPW];
-#ifdef GO2PI_DIAG_TILEOUTER  // previous order: each tile's 4 k-steps back to back
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        acc[i] = mfma4(cur[i].x, a[u].x, acc[i]);
-        acc[i] = mfma4(cur[i].y, a[u].y, acc[i]);
-        acc[i] = mfma4(cur[i].z, a[u].z, acc[i]);
-        acc[i] = mfma4(cur[i].w, a[u].w, acc[i]);
-        if (LOAD) {
-          __builtin_amdgcn_sched_barrier(0);
-          nxt[i] = ws.ld(vo[i], cn * csb);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-#else
-      // k-step outer, tile inner: consecutive MFMAs hit different accumulators,
-      // so one wave issues at the 32-cycle rate instead of waiting out the
-      // 40-cycle dependent-accumulator latency. Each accumulator still sees its
-      // k-steps in the same order, so results are bitwise unchanged. One
-      // fragment load after every 4th MFMA: TPW loads spread over 4*TPW MFMAs.
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-          acc[i] = mfma4(f4c(cur[i], j), f4c(a[u], j), acc[i]);
-          const int s = j * TPW + i;
-          if (LOAD && (s & 3) == 3) {
-            __builtin_amdgcn_sched_barrier(0);
-            nxt[s >> 2] = ws.ld(vo[s >> 2], cn * csb);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-#endif
-      if (LOAD) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
-      }
-    }
-  };
-  bool all = false;
-  for (int k = 0; k + 1 < NG; ++k) {
-    const int gn = g + 1 == NG ? 0 : g + 1;
-    handoff_wait(h, c0 + 4 * g, nw, lane, all);
-    group(c0 + 4 * g, c0 + 4 * gn, std::false_type{});
-    g = gn;
-  }
-  handoff_wait(h, c0 + 4 * g, nw, lane, all);
-  group(c0 + 4 * g, 0, std::true_type{});
-}
-
-// Contraction for one wave per SIMD (4 waves per workgroup): a wave owns TPW
-// tiles over the full K and nothing on its SIMD competes for the matrix pipe,
-// so the schedule must hide every latency by itself:
-//   * weight fragments stream RD chunks ahead through a 4-slot register ring
-//     (slot = chunk % 4): the fragment an MFMA consumes was issued >= RD - 1
-//     chunks (>= (RD - 1) * 4 * TPW MFMAs) earlier;
-//   * the A operand of chunk c + 1 is read from LDS during chunk c;
-//   * loads are spread one per 4 MFMAs (sched_barrier pins them in place).
-// The k-step / tile order is the same as dense_acc's, so every accumulator sees
-// its k-steps in the same order: results are bitwise those of dense_acc.
-// Requires C % 4 == 0 (K padded to 64) and C >= 4.
-template <int TPW, int RD>
-__device__ __forceinline__ void dense_acc_ring(const float *X, int xs, const float4 *__restrict__ W, int TL,
-                                               int t_first, int T, int C, int lane, f32x4 (&acc)[TPW]) {
-  static_assert(RD >= 1 && RD <= 3, "ring of 4 slots: at most 3 chunks ahead");
-  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  const WStream ws(W);
-  int vo[TPW];                // per-lane byte offset of each tile's fragment in chunk 0
-  const int csb = TL * 1024;  // bytes per chunk (all tiles)
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) vo[i] = (min(t_first + i, T - 1) * 64 + lane) * 16;
-  float4 f[4][TPW];
-  float4 a[2];
-#pragma unroll
-  for (int d = 0; d < RD; ++d)
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) f[d][i] = ws.ld(vo[i], d * csb);
-  a[0] = *reinterpret_cast<const float4 *>(xrow);
-  // one 4-chunk group; TAIL: the last one (no loads past C)
-  auto group = [&](int c0, auto tail_k) {
-    constexpr bool TAIL = decltype(tail_k)::value;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = c0 + u;
-      if (!(TAIL && u == 3)) a[(u + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
-      const bool LOAD = !(TAIL && u + RD >= 4);  // chunk c + RD exists (folded after unrolling)
-      constexpr int NS = 4 * TPW;                 // MFMAs per chunk
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-          acc[i] = mfma4(f4c(f[u][i], j), f4c(a[u & 1], j), acc[i]);
-          const int s = j * TPW + i;
-          if (LOAD && (s % (NS / TPW)) == (NS / TPW) - 1) {
-            __builtin_amdgcn_sched_barrier(0);
-            f[(u + RD) & 3][s / (NS / TPW)] = ws.ld(vo[s / (NS / TPW)], (c + RD) * csb);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-  };
-  int c0 = 0;
-  for (; c0 + 4 < C; c0 += 4) group(c0, std::false_type{});
-  group(c0, std::true_type{});
-}
-
-// Accumulator layout of the dense path ("output-major"): the weight fragment is
-// the MFMA's A operand and the activations its B operand, so D = W_tile . X^T
-// and lane l holds outputs n = 16t + 4(l >> 4) + r (r = 0..3) of robot l & 15:
-// four consecutive outputs of one robot, i.e. one float4 of its activation row.
-// (The product and the per-accumulator k order are those of X . W^T: results
-// are bitwise the same as with the operands the other way round.)
-
-// The bias is fetched before the contraction and added in the epilogue, so its
-// load latency hides behind the MFMA loop instead of delaying the first MFMA.
-template <int TPW>
-__device__ __forceinline__ void load_bias(float4 (&bv)[TPW], const float *__restrict__ bias, int t_first, int T,
-                                          int lane) {
-#pragma unroll
-  for (int i = 0; i < TPW; ++i)
-    bv[i] = *reinterpret_cast<const float4 *>(bias + min(t_first + i, T - 1) * 16 + ((lane >> 4) << 2));
-}
-
-// Epilogue of a hidden layer: bias + activation, one float4 per tile and lane to
-// the LDS activation row (one ds_write_b128 instead of four ds_write_b32); the
-// activated values also go to `keep` (head fusion consumes them from registers).
-// Epilogue of the final layer: bias + activation + post, valid rows/cols to HBM.
-template <int TPW, bool KEEP = false>
-__device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer &L, f32x4 (&acc)[TPW],
-                                            const float4 (&bv)[TPW], int t_first, int T, int lane, bool last,
-                                            float *Y, int ys, float *out, const CtlView ctl, int row0, int B,
-                                            float4 (&keep)[TPW]) {
-  const int rob = lane & 15, n0 = (lane >> 4) << 2;
-  with_act(L.act, [&](auto act_k) {
-    constexpr int ACT = decltype(act_k)::value;
-    const float alpha = L.alpha;
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      const int t = t_first + i;
-      if (t >= T) continue;
-      float4 v;
-      v.x = act_t<ACT>(alpha, acc[i][0] + bv[i].x);
-      v.y = act_t<ACT>(alpha, acc[i][1] + bv[i].y);
-      v.z = act_t<ACT>(alpha, acc[i][2] + bv[i].z);
-      v.w = act_t<ACT>(alpha, acc[i][3] + bv[i].w);
-      if (!last) {
-        *reinterpret_cast<float4 *>(Y + rob * ys + t * 16 + n0) = v;
-        if constexpr (KEEP) keep[i] = v;
-      } else {
-        const int row = row0 + rob;
-        if (row >= B) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = t * 16 + n0 + r;
-          if (n >= L.N) continue;
-          const float y = post_fn(P, f4c(v, r));
-          if (ctl.on) ctl_store(ctl, row, n, y);  // controller tick: action post-processing
-          else out[(size_t)row * L.N + n] = y;
-        }
-      }
-    }
-  });
-}
-
-// HT > 0: "head fusion". The final, narrow layer HL (HT <= 2 output tiles, e.g.
-// the 12 actions) is accumulated inside this layer: the wave's freshly stored
-// tiles are exactly its K-chunks of HL, so it multiplies them (read back from
-// LDS by the same wave) against HL's fragments, fetched before its MFMA loop.
-// Partials are summed across waves in a fixed order by head_finish (below).
-template <int TPW, int HT, int RD = 0>
-__device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int t_first, int T, int C, int lane, bool last, float *out,
-                                            const CtlView ctl, int row0, int B, const DevLayer *HL,
-                                            f32x4 (&hacc)[HT > 0 ? HT : 1], const Handoff &h, int g0, int nw) {
-  constexpr int HN = HT > 0 ? HT : 1;
-  f32x4 acc[TPW];
-  float4 bv[TPW];
-  float4 hw[HN][TPW];
-  load_bias<TPW>(bv, L.bias, t_first, T, lane);
-  if constexpr (HT > 0) {
-    const float4 *HW = reinterpret_cast<const float4 *>(HL->w);
-    const int HTL = HL->N_pad >> 4;  // head tiles (chunk-major fragments)
-#pragma unroll
-    for (int h = 0; h < HT; ++h)
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)min(t_first + i, T - 1) * HTL + h) * 64 + lane];
-  }
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef GO2PI_DIAG_CLOCK  // per-wave phase stamps inside layer 1: entry, contraction done, epilogue done
-  unsigned long long *st = (P.stamps && &L == &P.L[1] && lane == 0)
-                               ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * (threadIdx.x >> 6)
-                               : nullptr;
-  if (st) st[0] = __builtin_amdgcn_s_memtime();
-#endif
-  if constexpr (RD > 0)
-    dense_acc_ring<TPW, RD>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, C, lane, acc);
-  else
-    dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc, h, g0,
-                   nw);
-#ifdef GO2PI_DIAG_CLOCK
-  if (st) st[1] = __builtin_amdgcn_s_memtime();
-#endif
-  float4 yv[TPW];
-  dense_store<TPW, (HT > 0)>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, ctl, row0, B, yv);
-#ifdef GO2PI_DIAG_CLOCK
-  if (st) st[2] = __builtin_amdgcn_s_memtime();
-#endif
-  if constexpr (HT > 0) {
-    // the head's B operand for k-chunk t_first + i is exactly the float4 this
-    // lane just stored (its robot, k = 16t + 4(lane >> 4) + j): use the registers
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      if (t_first + i >= T) continue;
-#pragma unroll
-      for (int h = 0; h < HT; ++h) {
-        hacc[h] = mfma4(hw[h][i].x, yv[i].x, hacc[h]);
-        hacc[h] = mfma4(hw[h][i].y, yv[i].y, hacc[h]);
-        hacc[h] = mfma4(hw[h][i].z, yv[i].z, hacc[h]);
-        hacc[h] = mfma4(hw[h][i].w, yv[i].w, hacc[h]);
-      }
-    }
-  }
-}
-
-template <int TPW>
-__device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int t_first, int T, int C, int lane, bool last, float *out,
-                                            const CtlView ctl, int row0, int B) {
-  f32x4 none[1];
-  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none,
-                      Handoff{nullptr, 0, 1}, 0, 0);
-}
-
-// Tiles of a wide layer split over the NW waves (full K per wave), optionally
-// with the fused head (HT > 0). Barrier-free.
-template <int NW, int HT>
-__device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            int wave, int lane, bool last, float *out, const CtlView ctl, int row0,
-                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1],
-                                            const Handoff &h) {
-  const int T = L.N_pad >> 4, C = L.K_pad >> 4;
-  // largest tile group per pass: bounded so the accumulators fit the VGPR
-  // budget of NW waves per CU (512 / (NW/4) registers per lane)
-#ifdef GO2PI_DIAG_G2
-  constexpr int G = 2;  // variant: smaller tile groups (epilogue of one group beside MFMAs of the next)
-#else
-  constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
-#endif
-  // one wave per SIMD: the register-ring contraction (dense_acc_ring)
-  constexpr int RD = NW == 4 ? GO2PI_RING_RD : 0;
-  const int tpw = (T + NW - 1) / NW;
-  int t = wave * tpw;
-  const int t_end = min(t + tpw, T);
-  const int g0 = h.flags ? (wave * h.tpw) >> 2 : 0;  // the chunk group this wave produced itself
-  Handoff hh = h;  // prefetched fragments (hh.npre) belong to the first group only
-  for (; t + G <= t_end; t += G) {
-    dense_group<G, HT, RD>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
-    hh.npre = 0;
-  }
-  const int rem = t_end - t;
-  if (G > 4 && rem > 4)
-    dense_group<G, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
-  else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0,
-                                     NW);
-  else if (rem == 2)
-    dense_group<2, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
-  else if (rem == 1)
-    dense_group<1, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
-}
-
-// Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
-// partials go to LDS scratch; head_finish sums them after the layer barrier.
-template <int NW, int HT>
-__device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevLayer &L, const DevLayer &HL,
-                                                 const float *X, float *Y, int xs, f32x4 *scratch, int wave,
-                                                 int lane, int row0, int B, const Handoff &hin) {
-  f32x4 hacc[HT];
-#pragma unroll
-  for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc, hin);
-#pragma unroll
-  for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
-}
-
-template <int NW>
-__device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer &HL, const f32x4 *scratch, int wave,
-                                            int lane, float *out, const CtlView ctl, int row0, int B) {
-  const int T = HL.N_pad >> 4;
-  if (wave >= T) return;
-  f32x4 acc[1] = {scratch[(wave * NW) * 64 + lane]};
-  for (int w = 1; w < NW; ++w) acc[0] += scratch[(wave * NW + w) * 64 + lane];  // fixed order: deterministic
-  float4 bv[1];
-  load_bias<1>(bv, HL.bias, wave, T, lane);
-  float4 none[1];
-  dense_store<1>(P, HL, acc, bv, wave, T, lane, true, nullptr, 0, out, ctl, row0, B, none);
-}
-
-// One dense layer for the whole workgroup (NW waves). Contains barriers only in
-// the split-K branch, which every wave of the workgroup takes together.
-template <int NW>
-__device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
-                                            f32x4 *scratch, int wave, int lane, bool last, float *out,
-                                            const CtlView ctl, int row0, int B, const Handoff &hin) {
-  const int T = L.N_pad >> 4, C = L.K_pad >> 4;
-  if (T >= NW) {
-    f32x4 none[1];
-    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none, hin);
-  } else {
-    // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
-    const int ks = NW / T;
-    const int t = wave % T, s = wave / T;
-    f32x4 acc[1];
-    float4 bv[1];
-    load_bias<1>(bv, L.bias, t, T, lane);
-    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (s < ks) {
-      const int C4 = C >> 2;  // split on 4-chunk boundaries (dense_acc unrolls by 4)
-      const int c0 = 4 * ((s * C4) / ks), c1 = 4 * (((s + 1) * C4) / ks);
-      dense_acc<1>(X, xs, reinterpret_cast<const float4 *>(L.w), T, t, T, c0, c1, lane, acc);
-      if (s > 0) scratch[wave * 64 + lane] = acc[0];
-    }
-    __syncthreads();
-    if (s == 0) {
-      for (int s2 = 1; s2 < ks; ++s2) acc[0] += scratch[(t + s2 * T) * 64 + lane];
-      float4 none[1];
-      dense_store<1>(P, L, acc, bv, t, T, lane, last, Y, xs, out, ctl, row0, B, none);
-    }
-  }
-}
-
-// GRU cell (ONNX semantics, linear_before_reset = 1) for one 16-robot tile.
-// X: LDS rows [16][xs] holding x in columns [0, I_pad); Hs: LDS hidden rows
-// (stride xs). Writes h' to Y[:, 0:H]; the caller copies it back into Hs after
-// a barrier (other waves still read Hs as their MFMA A operand here).
-template <int GT>
-__device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
-                                          int t_first, int lane) {
-  const int Cx = G.I_pad >> 4, Ch = G.H >> 4, Cc = Cx + Ch;
-  const float4 *W = reinterpret_cast<const float4 *>(G.w);
-  const int col = lane & 15, r0 = (lane >> 4) << 2;
-  f32x4 z[GT], r[GT], nx[GT], nh[GT];
-  const WStream ws(W);
-  int vo[GT];  // per-lane byte offset of tile t_first + i's z fragment in chunk 0 (r: +1 KiB, n: +2 KiB)
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    const int j = (t_first + i) * 16 + col;
-    const float bz = G.bzr[j], br = G.bzr[G.H + j], bx = G.bh[j], bh = G.bh[G.H + j];
-    z[i] = f32x4{bz, bz, bz, bz};
-    r[i] = f32x4{br, br, br, br};
-    nx[i] = f32x4{bx, bx, bx, bx};
-    nh[i] = f32x4{bh, bh, bh, bh};
-    vo[i] = ((t_first + i) * 192 + lane) * 16;
-  }
-  const int csb = (G.H >> 4) * 192 * 16;  // bytes per chunk, chunk-major: [chunk][tile][gate][lane]
-  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
-  // One stream over the concatenated [x | h] chunks, scheduled like dense_acc:
-  // each gate fragment of chunk c+1 is loaded right after that gate's 4 MFMAs
-  // of chunk c (x chunks feed z, r, n_x; h chunks feed z, r, n_h).
-  float4 cz[GT], cr[GT], chh[GT];
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    cz[i] = ws.ld(vo[i], 0);
-    cr[i] = ws.ld(vo[i] + 1024, 0);
-    chh[i] = ws.ld(vo[i] + 2048, 0);
-  }
-  auto step = [&](int c, const float4 &a, f32x4 (&third)[GT], int cn) {
-    float4 nz[GT], nr[GT], nh3[GT];
-#ifndef GO2PI_DIAG_TILEOUTER
-    // k-step outer over the 3*GT independent gate accumulators (no back-to-back
-    // dependent MFMA; per-accumulator k order unchanged), one gate-fragment load
-    // after every 4th MFMA
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int i = 0; i < GT; ++i) {
-        z[i] = mfma4(f4c(a, j), f4c(cz[i], j), z[i]);
-        r[i] = mfma4(f4c(a, j), f4c(cr[i], j), r[i]);
-        third[i] = mfma4(f4c(a, j), f4c(chh[i], j), third[i]);
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int s = (j * GT + i) * 3 + g;
-          if ((s & 3) == 3) {
-            const int q = s >> 2, ti = q / 3, gi = q % 3;
-            __builtin_amdgcn_sched_barrier(0);
-            const float4 f = ws.ld(vo[ti] + 1024 * gi, cn * csb);
-            if (gi == 0) nz[ti] = f;
-            else if (gi == 1) nr[ti] = f;
-            else nh3[ti] = f;
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-#else
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.x, cz[i].x, z[i]);
-      z[i] = mfma4(a.y, cz[i].y, z[i]);
-      z[i] = mfma4(a.z, cz[i].z, z[i]);
-      z[i] = mfma4(a.w, cz[i].w, z[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nz[i] = ws.ld(vo[i], cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-      r[i] = mfma4(a.x, cr[i].x, r[i]);
-      r[i] = mfma4(a.y, cr[i].y, r[i]);
-      r[i] = mfma4(a.z, cr[i].z, r[i]);
-      r[i] = mfma4(a.w, cr[i].w, r[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nr[i] = ws.ld(vo[i] + 1024, cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-      third[i] = mfma4(a.x, chh[i].x, third[i]);
-      third[i] = mfma4(a.y, chh[i].y, third[i]);
-      third[i] = mfma4(a.z, chh[i].z, third[i]);
-      third[i] = mfma4(a.w, chh[i].w, third[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nh3[i] = ws.ld(vo[i] + 2048, cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      cz[i] = nz[i];
-      cr[i] = nr[i];
-      chh[i] = nh3[i];
-    }
-    (void)c;
-  };
-  for (int c = 0; c < Cx; ++c) step(c, *reinterpret_cast<const float4 *>(xrow + c * 16), nx, c + 1);
-  for (int c = 0; c < Ch; ++c)
-    step(Cx + c, *reinterpret_cast<const float4 *>(hrow + c * 16), nh, min(Cx + c + 1, Cc - 1));
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    const int j = (t_first + i) * 16 + col;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = r0 + e;
-      const float zg = sigmoid_fast(z[i][e]);
-      const float rg = sigmoid_fast(r[i][e]);
-      const float hn = 2.f * sigmoid_fast(2.f * (nx[i][e] + rg * nh[i][e])) - 1.f;  // tanh, ~1e-7 abs
-      const float ho = Hs[row * xs + j];
-      Y[row * xs + j] = (1.f - zg) * hn + zg * ho;
-    }
-  }
-}
-
-template <int NW>
-__device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
-                                         int wave, int lane) {
-  const int Ht = G.H >> 4;
-  const int tpw = (Ht + NW - 1) / NW;
-  int t = wave * tpw;
-  const int t_end = min(t + tpw, Ht);
-  constexpr int GM = NW >= 16 ? 1 : (NW >= 8 ? 2 : 4);  // VGPR budget per wave count
-  for (; t + GM <= t_end; t += GM) gru_group<GM>(G, X, Hs, Y, xs, t, lane);
-  if (GM > 2)
-    for (; t + 2 <= t_end; t += 2) gru_group<2>(G, X, Hs, Y, xs, t, lane);
-  for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
-}
-
-// ---------------------------------------------------------------------------
-// Uniform-MLP pipeline at one wave per SIMD (4 waves per workgroup; the engine
-// selects it for policies whose hidden layers are all 64 * TPW wide, TPW = 2, 4
-// or 8, with the final layer fused as the head). Wave w owns output tiles
-// [t0, t0 + TPW) of EVERY hidden layer, t0 = w * TPW, over the full K.
-//
-//  * Weight stream: a 4-slot register ring of MFMA A-operand fragments (slot =
-//    consumption index k & 3) filled RD chunks ahead by buffer loads, one per 4
-//    MFMAs. It runs across layer boundaries: the tail of layer l issues layer
-//    l + 1's first RD chunks, layer 0's go out before the observation barrier.
-//  * Register hand-off: the k-chunks of layer l + 1 that a wave produced itself
-//    (chunks t0 .. t0 + TPW - 1: its own output tiles of layer l) are consumed
-//    FIRST and straight from registers: the epilogue value of tile t0 + i (one
-//    float4 per lane = the MFMA B operand for that chunk) feeds chunk i, and the
-//    epilogue of tile i + 1 is interleaved with chunk i's MFMAs (sched_group
-//    pattern). Each tile also goes to LDS for the other waves. The remaining
-//    chunks are read from LDS in rotated order (t0 + k mod C) after ONE wait on
-//    the other waves' per-layer flags (LDS words) — no workgroup barrier between
-//    layers, and the epilogue runs beside the MFMA pipe instead of in front of it.
-//  * WAR safety of the two LDS activation buffers: a wave writes layer l + 1's
-//    tiles into the buffer layer l read only after it has seen every wave's
-//    layer-l flag, which each wave sets after it finished reading that buffer
-//    (its layer l contraction).
-// Numerics: every accumulator is an fp32 fma chain over its K in a fixed
-// per-output order (own chunks first, then rotated): identical for every robot
-// row, so sharded and unsharded runs stay bitwise equal; the order differs from
-// the generic body's, which the tolerance-based parity tests cover.
-
-// one chunk (16 k) of MFMAs for the wave's TPW tiles: A = ring slot S, B = b
-// (4 k-steps in its components); LOAD: after every 4th MFMA the next fragment of
-// the chunk RD ahead goes into slot (S + RD) & 3 at byte offset soff of ws. PIN:
-// sched_barrier around each load (the LDS phase); otherwise the caller's
-// sched_group pattern places it (the own phase).
-// Load spacing: one fragment load after every LSP-th MFMA, so the chunk's TPW
-// loads are issued over its first LSP * TPW MFMAs (the earlier they go out, the
-// longer the last tile's fragment has before its MFMA in the next chunk).
-#if defined(GO2PI_DIAG_LSP1)
-#define GO2PI_W4_LSP 1
-#elif defined(GO2PI_DIAG_LSP4)
-#define GO2PI_W4_LSP 4
-#elif !defined(GO2PI_W4_LSP)
-#define GO2PI_W4_LSP 2
-#endif
-template <int TPW, int S, int RD, bool LOAD, bool PIN>
-__device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b, const WStream &ws,
-                                         const int (&vo)[TPW], int soff) {
-  constexpr int LSP = GO2PI_W4_LSP;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      acc[i] = mfma4(f4c(f[S][i], j), f4c(b, j), acc[i]);
-      const int s = j * TPW + i;
-      if (LOAD && s % LSP == LSP - 1 && s / LSP < TPW) {
-        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-        f[(S + RD) & 3][s / LSP] = ws.ld(vo[s / LSP], soff);
-        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-}
-
-// bias + activation of one 16 x 16 tile (output-major: one float4 per lane)
-template <int ACT>
-__device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const float4 &bv) {
-  float4 v;
-  v.x = act_t<ACT>(alpha, acc[0] + bv.x);
-  v.y = act_t<ACT>(alpha, acc[1] + bv.y);
-  v.z = act_t<ACT>(alpha, acc[2] + bv.z);
-  v.w = act_t<ACT>(alpha, acc[3] + bv.w);
-  return v;
-}
-
-// One own-phase chunk: the MFMAs of chunk I (B operand b = the epilogue value of
-// the previous layer's tile t0 + I, from registers) with the epilogue of tile
-// I + 1 (accumulator pa, bias pb) woven between them when NEXT. The epilogue is
-// cut into short dependent stages, one after each MFMA from the 4th on (per
-// element: bias add; for Elu also x*log2(e), exp2, alpha*(e-1), select), each
-// pinned by sched_barrier, so its VALU issues in the MFMA pipe's shadow and every
-// dependent stage sits >= 4 MFMAs after its producer. Other activations compute
-// the whole epilogue behind the chunk's MFMAs. Results are bitwise those of
-// w4_epi (the same operations in the same order per element).
-template <int TPW, int S, int RD, int ACT, bool NEXT>
-__device__ __forceinline__ void w4_own_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b,
-                                             const WStream &ws, const int (&vo)[TPW], int soff, const f32x4 &pa,
-                                             const float4 &pb, float alpha, float4 &vn) {
-  constexpr int NM = 4 * TPW;                // MFMAs in the chunk
-  constexpr int NSTG = ACT == 1 ? 5 : 1;    // stages per element
-  constexpr int NS = 4 * NSTG;              // stage slots (4 elements)
-  constexpr int FIRST = NM >= 8 ? 3 : 0;    // first MFMA followed by a stage
-  constexpr int SLOTS = NM - FIRST;
-  constexpr int PER = (NS + SLOTS - 1) / SLOTS;  // stages after each MFMA
-  float t[4], u[4];
-  auto stage = [&](auto q_k) {
-    constexpr int Q = decltype(q_k)::value;  // stage index: element Q % 4, step Q / 4
-    constexpr int E = Q & 3, ST = Q >> 2;
-    // (the empty asm on each stage's result keeps the stages where they are put:
-    // otherwise the SLP vectorizer merges the four elements' stages into packed
-    // ops at the first position)
-    if constexpr (ACT == 1) {
-      if constexpr (ST == 0) {
-        t[E] = pa[E] + f4c(pb, E);
-        asm volatile("" : "+v"(t[E]));
-      } else if constexpr (ST == 1) {
-        u[E] = t[E] * 1.4426950408889634f;
-        asm volatile("" : "+v"(u[E]));
-      } else if constexpr (ST == 2) {
-        u[E] = __builtin_amdgcn_exp2f(u[E]);
-        asm volatile("" : "+v"(u[E]));
-      } else if constexpr (ST == 3) {
-        u[E] = alpha * (u[E] - 1.f);
-        asm volatile("" : "+v"(u[E]));
-      } else {
-        float r = t[E] > 0.f ? t[E] : u[E];
-        asm volatile("" : "+v"(r));
-        if constexpr (E == 0) vn.x = r;
-        else if constexpr (E == 1) vn.y = r;
-        else if constexpr (E == 2) vn.z = r;
-        else vn.w = r;
-      }
-    } else {
-      const float r = act_t<ACT>(alpha, pa[E] + f4c(pb, E));
-      if constexpr (E == 0) vn.x = r;
-      else if constexpr (E == 1) vn.y = r;
-      else if constexpr (E == 2) vn.z = r;
-      else vn.w = r;
-    }
-  };
-  auto stages_after = [&](auto m_k) {
-    constexpr int M = decltype(m_k)::value;
-    if constexpr (NEXT && M >= FIRST) {
-      constexpr int Q0 = (M - FIRST) * PER;
-      [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((Q0 + P < NS ? stage(std::integral_constant<int, (Q0 + P < NS ? Q0 + P : 0)>{}) : void()), ...);
-      }(std::make_integer_sequence<int, PER>{});
-    }
-  };
-  [&]<int... M>(std::integer_sequence<int, M...>) {
-    (([&] {
-       constexpr int J = M / TPW, I = M % TPW;
-       acc[I] = mfma4(f4c(f[S][I], J), f4c(b, J), acc[I]);
-       if constexpr ((M & 3) == 3) f[(S + RD) & 3][M >> 2] = ws.ld(vo[M >> 2], soff);
-       stages_after(std::integral_constant<int, M>{});
-       __builtin_amdgcn_sched_barrier(0);
-     }()),
-     ...);
-  }(std::make_integer_sequence<int, NM>{});
-}
-
-// Chunks k in [k0, C) of a layer from the LDS activation rows X, chunk
-// c = (kb + k) mod C, ring slots by k (k0 % 4 == K0S; C % 4 == 0). Groups of 4
-// chunks, the last one NT chunks long ((C - k0) % 4 == NT % 4). NEXT: past the
-// layer's own chunks the ring loads NL's chunks (kbn + d) mod Cn, d < RD (NL's
-// consumption order).
-template <int TPW, int RD, int K0S, int NT, bool NEXT>
-__device__ __forceinline__ void w4_lds_phase(const float *X, int xs, int lane, int C, int kb, int k0,
-                                             const WStream &ws, int csb, const WStream &wn, int csn, int kbn, int Cn,
-                                             const int (&vo)[TPW], f32x4 (&acc)[TPW], float4 (&f)[4][TPW]) {
-  static_assert((K0S == 0 || K0S == 2) && (NT == 2 || NT == 4) && RD <= NT, "phase shape");
-  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
-  auto chunk_of = [&](int k) {
-    const int c = kb + k;
-    return c >= C ? c - C : c;
-  };
-  auto next_of = [&](int d) {
-    const int c = kbn + d;
-    return c >= Cn ? c - Cn : c;
-  };
-  float4 a[2];
-  a[0] = *reinterpret_cast<const float4 *>(xrow + chunk_of(k0) * 16);
-  // one group of 4 chunks from k = g (slots K0S .. K0S + 3, mod 4); TAIL: the last
-  auto group = [&](int g, auto tail_k) {
-    constexpr bool TAIL = decltype(tail_k)::value;
-    auto step = [&](auto u_k) {
-      constexpr int U = decltype(u_k)::value;
-      constexpr int S = (K0S + U) & 3;
-      constexpr int N = TAIL ? NT : 4;  // chunks in this group
-      if constexpr (U < N) {
-        const int k = g + U;
-        if (U + 1 < N || !TAIL) a[(U + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + chunk_of(k + 1) * 16);
-        constexpr bool OWN = !(TAIL && U + RD >= N);  // chunk k + RD is this layer's
-        if constexpr (OWN)
-          w4_chunk<TPW, S, RD, true, true>(acc, f, a[U & 1], ws, vo, chunk_of(k + RD) * csb);
-        else if constexpr (NEXT)
-          w4_chunk<TPW, S, RD, true, true>(acc, f, a[U & 1], wn, vo, next_of(U + RD - N) * csn);
-        else
-          w4_chunk<TPW, S, RD, false, true>(acc, f, a[U & 1], ws, vo, 0);
-      }
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-  };
-  int g = k0;
-  for (; g + NT < C; g += 4) group(g, std::false_type{});
-  group(g, std::true_type{});
-}
-
-// Bounded wait until every OTHER wave has published epoch ep (an LDS word per
-// wave). A protocol failure must not hang the GPU: past the bound the kernel
-// reports through P.err (the engine raises it at the next sync) and goes on.
-__device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int lane, unsigned *err) {
-  for (int it = 0;; ++it) {
-    const int f = lane < 4 && lane != wave ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP)
-                                           : ep;
-    if (__ballot(f < ep) == 0ull) break;
-    if (it == (1 << 22)) {  // ~ seconds
-      if (lane == 0 && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");  // the LDS reads of the other waves' tiles stay after the wait
-}
-
-// GRU cell as the pipeline's front stage (one wave per SIMD): wave w owns hidden
-// tiles [w * GT, (w + 1) * GT) (H = 64 * GT) over the concatenated [x | h] chunks
-// (Cx = I_pad / 16 and Ch = H / 16, both multiples of 4: the engine pads I to 64).
-// The same register ring and buffer-load stream as the dense layers (RD = 1,
-// loads every 2 MFMAs), B operand one chunk ahead from LDS, output-major
-// accumulators (the gate fragment is the A operand): lane l holds units
-// 16t + 4(l >> 4) + e of robot l & 15, so the old h and the new h' move as one
-// float4 per tile. Gate math as gru_group (ONNX GRU, linear_before_reset = 1).
-// h' goes to Y rows and to hn (registers) for the caller. The caller has issued
-// the direct-to-LDS loads of x and h; this stage issues its first chunk's
-// fragments, waits for everything OLDER than them (the LDS-DMA), then barriers,
-// so the fragment latency overlaps the staging. Gate biases are added after the
-// contraction (accumulators start at zero), so their loads wait nowhere.
-template <int GT>
-__device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
-                                       int lane, float4 (&hn)[GT], unsigned long long *st = nullptr) {
-#ifdef GO2PI_DIAG_CLOCK  // GRU stage marks (wave 0): 43 entry, 44 contraction done, 45 epilogue done
-  if (st && wave == 0 && lane == 0) st[43] = __builtin_amdgcn_s_memtime();
-#endif
-  constexpr int NF = 3 * GT;  // gate fragments per chunk
-  constexpr int NM = 4 * NF;  // MFMAs per chunk
-  const int Cx = G.I_pad >> 4, Ch = G.H >> 4;
-  const int t0 = wave * GT, u0 = (lane >> 4) << 2;
-  const WStream ws(G.w);
-  const int csb = Ch * 3 * 1024;  // bytes per chunk (all tiles, three gates)
-  int vo[GT];                     // per-lane byte offset of tile t0 + i's z fragment in chunk 0 (r +1 KiB, n +2 KiB)
-#pragma unroll
-  for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 3 * 64 + lane) * 16;
-  float4 f[4][NF];
-  asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
-#pragma unroll
-  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
-  wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
-  f32x4 z[GT], r[GT], nx[GT], nh[GT];
-  float4 bz[GT], br[GT], bx[GT], bh[GT];
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    const int j = (t0 + i) * 16 + u0;
-    bz[i] = *reinterpret_cast<const float4 *>(G.bzr + j);
-    br[i] = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
-    bx[i] = *reinterpret_cast<const float4 *>(G.bh + j);
-    bh[i] = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
-    z[i] = r[i] = nx[i] = nh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const float *xrow = X + (lane & 15) * xs + u0;
-  const float *hrow = Hs + (lane & 15) * xs + u0;
-  float4 a[2];
-  a[0] = *reinterpret_cast<const float4 *>(xrow);
-  // chunk c (slot S = c & 3); XPH: an x chunk (the third gate accumulates n_x, else
-  // n_h); NEXT: chunk c + 1 exists (its B operand and fragments are fetched here);
-  // NX: chunk c + 1 is an x chunk (else an h chunk). One fixed source row per
-  // instantiation keeps the B-operand read a single ds_read_b128.
-  auto chunk = [&](auto s_k, auto xph_k, auto next_k, auto nx_k, int c) {
-    constexpr int S = decltype(s_k)::value;
-    constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
-    if constexpr (NEXT) {
-      if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
-      else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (c + 1 - Cx) * 16);
-    }
-    const float4 b = a[S & 1];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      const int jk = m / NF, i = (m % NF) / 3, g = m % 3;
-      const float wv = f4c(f[S][i * 3 + g], jk), bk = f4c(b, jk);
-      if (g == 0) z[i] = mfma4(wv, bk, z[i]);
-      else if (g == 1) r[i] = mfma4(wv, bk, r[i]);
-      else if (XPH) nx[i] = mfma4(wv, bk, nx[i]);
-      else nh[i] = mfma4(wv, bk, nh[i]);
-      if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
-        const int q = m >> 1;
-        __builtin_amdgcn_sched_barrier(0);
-        f[(S + 1) & 3][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, (c + 1) * csb);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  int c = 0;
-  for (; c + 4 < Cx; c += 4) {
-    chunk(I0{}, T_{}, T_{}, T_{}, c);
-    chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
-    chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
-    chunk(I3{}, T_{}, T_{}, T_{}, c + 3);
-  }
-  chunk(I0{}, T_{}, T_{}, T_{}, c);
-  chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
-  chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
-  chunk(I3{}, T_{}, T_{}, F_{}, c + 3);  // the next chunk is the first h chunk
-  for (c = Cx; c + 4 < Cx + Ch; c += 4) {
-    chunk(I0{}, F_{}, T_{}, F_{}, c);
-    chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
-    chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
-    chunk(I3{}, F_{}, T_{}, F_{}, c + 3);
-  }
-  chunk(I0{}, F_{}, T_{}, F_{}, c);
-  chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
-  chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
-  chunk(I3{}, F_{}, F_{}, F_{}, c + 3);
-#ifdef GO2PI_DIAG_CLOCK
-  if (st && wave == 0 && lane == 0) st[44] = __builtin_amdgcn_s_memtime();
-#endif
-  float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    const float4 ho = *reinterpret_cast<const float4 *>(hrow + (t0 + i) * 16);
-    float o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float zg = sigmoid_fast(z[i][e] + f4c(bz[i], e));
-      const float rg = sigmoid_fast(r[i][e] + f4c(br[i], e));
-      const float nxe = nx[i][e] + f4c(bx[i], e), nhe = nh[i][e] + f4c(bh[i], e);
-      const float hv = 2.f * sigmoid_fast(2.f * (nxe + rg * nhe)) - 1.f;  // tanh, ~1e-7 abs
-      o[e] = (1.f - zg) * hv + zg * f4c(ho, e);
-    }
-    hn[i] = make_float4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<float4 *>(yrow + i * 16) = hn[i];
-  }
-#ifdef GO2PI_DIAG_CLOCK
-  if (st && wave == 0 && lane == 0) st[45] = __builtin_amdgcn_s_memtime();
-#endif
-}
-
-// One policy step of the pipeline (the observation tile is being staged into bufA).
-// X0: layer 0's input rows (the observation tile, or a GRU's h'); Y0: the other
-// activation buffer (layer 0's outputs)
-template <int TPW, int HT, bool CTL>
-__device__ __forceinline__ void w4_step(const DevProgram &P, float *X0, float *Y0, int S, f32x4 *scratch,
-                                        int *flags, float *lbias, int &ep, int wave, int lane, float *ac,
-                                        const CtlView cv, int row0, int B, const DevCtl &ctl, const CtlLds &CL,
-                                        int step) {
-  constexpr int RD = GO2PI_W4_RD(TPW);
-  constexpr int CH = 4 * TPW;  // k-chunks of every layer after the first
-  // register hand-off between layers for 4 and 8 tiles per wave; at 2 tiles per
-  // wave (a 128-wide policy such as the shipped model) a layer's own phase is too
-  // short to cover the other waves' epilogues, and an epilogue + barrier + natural
-  // chunk order measured faster (9.9 vs 11.0 us per 4096-robot step)
-  constexpr bool HO = TPW >= 4;
-  const int t0 = wave * TPW;
-  const int kb1 = HO ? t0 : 0;  // first k-chunk of every layer after the first
-  const int nh = P.nl - 1;  // hidden layers; P.L[nh] is the fused head
-  int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
-  // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
-  // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
-  // weight stream, whose waits would otherwise cover them); the head's bias to registers
-  if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
-  float4 hbv[1];
-  load_bias<1>(hbv, P.L[nh].bias, wave < HT ? wave : 0, P.L[nh].N_pad >> 4, lane);
-  float4 f[4][TPW];
-  asm volatile("" ::: "memory");  // the DMA and bias loads stay ahead of the ring's first loads
-  {
-    const WStream w0(P.L[0].w);
-    const int cs0 = (P.L[0].N_pad >> 4) * 1024;
-#pragma unroll
-    for (int d = 0; d < RD; ++d)
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) f[d][i] = w0.ld(vo[i], d * cs0);
-  }
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 42] = __builtin_amdgcn_s_memtime();
-#endif
-  // layer 0's input rows are complete in X0 and the biases in LDS (this wave's
-  // direct-to-LDS loads, older than the ring's); the ring's loads stay in flight
-  wg_barrier_vm<RD * TPW>();
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
-#endif
-  if constexpr (CTL) {
-    if (ctl.status && (int)threadIdx.x < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + threadIdx.x] = CL.nanf[threadIdx.x];
-#ifdef GO2PI_DIAG_CLOCK
-    if (threadIdx.x == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
-#endif
-  }
-  // the head's fragments (final layer, fused): fetched before the last hidden layer's LDS phase
-  float4 hw[HT][TPW];
-  auto load_head = [&](const DevLayer &) {
-    const DevLayer &HL = P.L[nh];
-    const float4 *HW = reinterpret_cast<const float4 *>(HL.w);
-    const int HTL = HL.N_pad >> 4;
-#pragma unroll
-    for (int h = 0; h < HT; ++h)
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) hw[h][i] = HW[((size_t)(t0 + i) * HTL + h) * 64 + lane];
-  };
-  if (nh == 1) load_head(P.L[0]);
-  // layer 0: the observation tile, natural chunk order; the tail fetches layer 1's own chunks
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float *brow = lbias + t0 * 16 + ((lane >> 4) << 2);  // this lane's bias float4 of tile t0, layer 0
-  float4 bv[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) bv[i] = *reinterpret_cast<const float4 *>(brow + i * 16);
-  {
-    const DevLayer &L = P.L[0];
-    const DevLayer &NL = P.L[nh > 1 ? 1 : 0];
-    const WStream ws(L.w), wn(NL.w);
-    if (nh > 1)
-      w4_lds_phase<TPW, RD, 0, 4, true>(X0, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn,
-                                     (NL.N_pad >> 4) * 1024, kb1, CH, vo, acc, f);
-    else
-      w4_lds_phase<TPW, RD, 0, 4, false>(X0, S, lane, L.K_pad >> 4, 0, 0, ws, (L.N_pad >> 4) * 1024, wn, 0, 0, 1, vo,
-                                      acc, f);
-  }
-#ifdef GO2PI_DIAG_CLOCK  // pipeline stamps: 6 + l = wave 0 done with hidden layer l, 6 + nh = head barrier;
-                         // 16 + 3w + min(l, 2) = wave w done with hidden layer l
-  if (lane == 0 && P.stamps && step == 0) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave] = __builtin_amdgcn_s_memtime();
-    if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6] = __builtin_amdgcn_s_memtime();
-  }
-#endif
-  float *Y = Y0;  // where the previous layer's activations go
-  for (int l = 1; l < nh; ++l) {
-    const DevLayer &PL = P.L[l - 1], &L = P.L[l];
-    const bool more = l + 1 < nh;
-    const DevLayer &NL = P.L[more ? l + 1 : l];
-    const WStream ws(L.w), wn(NL.w);
-    const int csb = (L.N_pad >> 4) * 1024, csn = (NL.N_pad >> 4) * 1024;
-    f32x4 accn[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) accn[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 bvn[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) bvn[i] = *reinterpret_cast<const float4 *>(brow + l * CH * 16 + i * 16);
-    float *yrow = Y + (lane & 15) * S + t0 * 16 + ((lane >> 4) << 2);
-    const float alpha = PL.alpha;
-    // publish this wave's layer l-1 tiles (after its own LDS stores) for the other waves
-    auto publish = [&] {
-      ++ep;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
-      if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-#ifdef GO2PI_DIAG_CLOCK  // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
-    unsigned long long *sub =
-        (lane == 0 && P.stamps && step == 0 && l == 1) ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 28 + 3 * wave
-                                                        : nullptr;
-#endif
-#ifdef GO2PI_DIAG_WEAVE
-    // variant (diagnostics): layer l-1's epilogue of tile i+1 woven between layer l's
-    // MFMAs of chunk t0+i (measured slower: the woven VALU stretches the MFMA gaps)
-    with_act(PL.act, [&](auto act_k) {
-      constexpr int ACT = decltype(act_k)::value;
-      float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
-      *reinterpret_cast<float4 *>(yrow) = v;
-      auto own = [&](auto i_k) {
-        constexpr int I = decltype(i_k)::value;
-        const int cl = (t0 + I + RD) & (CH - 1);  // chunk loaded into slot (I + RD) & 3
-        constexpr int IN = I + 1 < TPW ? I + 1 : I;
-        float4 vn = v;
-        w4_own_chunk<TPW, (I & 3), RD, ACT, (I + 1 < TPW)>(accn, f, v, ws, vo, cl * csb, acc[IN], bv[IN], alpha,
-                                                           vn);
-        if constexpr (I + 1 < TPW) {
-          v = vn;
-          *reinterpret_cast<float4 *>(yrow + (I + 1) * 16) = v;
-        }
-      };
-      [&]<int... I>(std::integer_sequence<int, I...>) {
-        (own(std::integral_constant<int, I>{}), ...);
-      }(std::make_integer_sequence<int, TPW>{});
-    });
-    publish();
-#else
-    // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
-    // publish, then layer l's MFMAs over those chunks with the B operand from registers
-    // (!HO: the epilogue to LDS, then a workgroup barrier)
-    with_act(PL.act, [&](auto act_k) {
-      constexpr int ACT = decltype(act_k)::value;
-      float4 v[TPW];
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
-#ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
-      if (sub) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 46 + wave] = __builtin_amdgcn_s_memtime();
-#endif
-      if constexpr (HO) {
-        publish();
-        [&]<int... I>(std::integer_sequence<int, I...>) {
-          (w4_chunk<TPW, (I & 3), RD, true, true>(accn, f, v[I], ws, vo, ((t0 + I + RD) & (CH - 1)) * csb), ...);
-        }(std::make_integer_sequence<int, TPW>{});
-      }
-    });
-    if constexpr (!HO) __syncthreads();
-#endif
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[0] = __builtin_amdgcn_s_memtime();
-#endif
-    if constexpr (HO) w4_wait(flags, wave, ep, lane, P.err);
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[1] = __builtin_amdgcn_s_memtime();
-#endif
-    // LDS phase: the other waves' chunks, rotated order from t0 + TPW
-    constexpr int K0 = HO ? TPW : 0;                             // first chunk index of the LDS phase
-    constexpr int NT = (CH - K0) % 4 ? (CH - K0) % 4 : 4;       // chunks in the LDS phase's last group
-    if (more) {
-      w4_lds_phase<TPW, RD, (K0 & 3), NT, true>(Y, S, lane, CH, kb1, K0, ws, csb, wn, csn, kb1, CH, vo, accn, f);
-    } else {
-      load_head(L);  // the head's fragments, behind the last LDS phase
-      w4_lds_phase<TPW, RD, (K0 & 3), NT, false>(Y, S, lane, CH, kb1, K0, ws, csb, wn, csn, 0, 1, vo, accn, f);
-    }
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[2] = __builtin_amdgcn_s_memtime();
-#endif
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      acc[i] = accn[i];
-      bv[i] = bvn[i];
-    }
-    Y = Y == X0 ? Y0 : X0;
-#ifdef GO2PI_DIAG_CLOCK
-    if (lane == 0 && P.stamps && step == 0 && l < 8) {
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave + (l < 3 ? l : 2)] = __builtin_amdgcn_s_memtime();
-      if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-    }
-#endif
-  }
-  // the last hidden layer's epilogue feeds the head from registers (no LDS copy)
-  {
-    const DevLayer &PL = P.L[nh - 1];
-    f32x4 hacc[HT];
-#pragma unroll
-    for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float alpha = PL.alpha;
-    with_act(PL.act, [&](auto act_k) {
-      constexpr int ACT = decltype(act_k)::value;
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        const float4 v = w4_epi<ACT>(alpha, acc[i], bv[i]);
-#pragma unroll
-        for (int h = 0; h < HT; ++h) {
-          hacc[h] = mfma4(hw[h][i].x, v.x, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].y, v.y, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].z, v.z, hacc[h]);
-          hacc[h] = mfma4(hw[h][i].w, v.w, hacc[h]);
-        }
-      }
-    });
-#pragma unroll
-    for (int h = 0; h < HT; ++h) scratch[(h * 4 + wave) * 64 + lane] = hacc[h];
-  }
-  __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0 && nh < 9) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + nh] = __builtin_amdgcn_s_memtime();
-#endif
-  if (wave < HT) {  // head tile `wave`: the four waves' partials in a fixed order, bias, final store
-    f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
-#pragma unroll
-    for (int w = 1; w < 4; ++w) hs[0] += scratch[(wave * 4 + w) * 64 + lane];
-    float4 none[1];
-    dense_store<1>(P, P.L[nh], hs, hbv, wave, HT, lane, true, nullptr, 0, ac, cv, row0, B, none);
-  }
-}
-
-// Body of the batched kernel. CTL: controller tick (steps == 1) — the
-// observation is assembled from raw robot state (ctl_assemble) instead of
-// read, and the final layer's store is the action post-processing (ctl_store).
-template <int NW, bool CTL, int W4T = 0, int W4H = 0>
-__device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
-                                           float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
-                                           const DevCtl ctl) {
-  extern __shared__ float4 lds4[];
-  float *lds = reinterpret_cast<float *>(lds4);
-  const int S = P.lds_stride;
-  float *bufA = lds;
-  float *bufB = lds + GO2PI_TILE_ROWS * S;
-  float *bufH = lds + 2 * GO2PI_TILE_ROWS * S;  // only with a GRU
-  f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
-  constexpr int NT = NW * 64;
-  const int H = P.gru.H;
-#ifdef GO2PI_DIAG_PRIO  // variant: static priority for the second-dispatched half of the waves
-  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-  // Touch every layer descriptor up front: one burst of scalar loads warms the
-  // scalar cache, so each layer's start does not pay a K$ miss on its fields
-  // (measured: layer entry ~990 -> ~740 cycles after the barrier).
-  if constexpr (W4T > 0) {
-    // pipeline: no warm-up (holding every descriptor in SGPRs spilled them to VGPR
-    // lanes; the fields are read where needed and hit the scalar cache after the
-    // first layer)
-  } else {
-    int d = 0;
-    for (int l = 0; l < P.nl; ++l) d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w;
-    asm volatile("" ::"s"(d));  // consumes the loads; no side effect
-  }
-#ifdef GO2PI_DIAG_CLOCK  // init sub-phases: 40 descriptors warm, 41 observation loads issued, 42 pipeline barrier reached
-  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 40] = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 1] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
-
-  // controller tick: this tile's raw inputs staged in LDS behind the scratch
-  // region (one burst of direct-to-LDS loads), then assembled from there
-  // per-wave layer hand-off flags (Handoff) behind the scratch region, cleared
-  // here; every path passes a workgroup barrier before the first layer
-  float *after_scratch = lds + (2 + P.has_gru) * GO2PI_TILE_ROWS * S + 256 * NW * (P.head_fuse > 1 ? P.head_fuse : 1);
-  int *flags = reinterpret_cast<int *>(after_scratch);
-  if (tid < NW) flags[tid] = 0;
-  int ep = 0;  // hand-offs published so far (identical in every wave)
-  // (the pipeline's bias copy sits between the flags and the controller-tick region)
-  float *lbias = after_scratch + GO2PI_FLAG_FLOATS;
-  const CtlLds CL = ctl_lds(lbias + P.w4_bias, GO2PI_TILE_ROWS, P.in_dim);
-  CtlView cv{};
-  CtlQ cq{};
-  if constexpr (CTL) {
-    cq = ctl_q(ctl);
-    cv = ctl_view(ctl, CL, row0);
-    ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
-    lds_dma_wait();
-    __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-    if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 5] = __builtin_amdgcn_s_memtime();
-#endif
-  }
-  // plain observation rows with no prologue arithmetic are staged by direct-to-LDS
-  // loads (needs whole 64-column chunks to fit the LDS row)
-  const bool glds_obs = !CTL && !P.pre_sub && !P.pre_div && !(P.obs_clip > 0.f) && ((P.in_pad + 63) & ~63) <= S;
-  auto stage_obs = [&](int step) {
-    if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
-      if constexpr (NW == 4)
-        ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
-                                ctl.obs + (size_t)row0 * P.in_dim, tid, NT);
-      else
-        ctl_assemble<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
-                           ctl.obs + (size_t)row0 * P.in_dim, wave, lane, NW);
-    } else if (W4T > 0 && glds_obs) {
-      // pipeline: wave w stages rows w, w + 4, w + 8, w + 12 in whole 64-column
-      // chunks (in_pad is a GRU's input width, not always a multiple of 64);
-      // per-lane source pointers are formed once, so the loop carries no scalar
-      // reloads between the direct-to-LDS loads
-      const int in_dim = P.in_dim, nch = (P.in_pad + 63) >> 6;
-      const float *ob = obs + (size_t)step * B * in_dim;
-      const float *zero = P.zero + lane;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wave + 4 * i, row = row0 + r;
-        const float *rp = ob + (size_t)row * in_dim + lane;
-        for (int c = 0; c < nch; ++c) {
-          const float *src = (row < B && c * 64 + lane < in_dim) ? rp + c * 64 : zero;
-          __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
-        }
-      }
-    } else if (glds_obs) {
-      // one direct-to-LDS load per (row, 64-column chunk): the tile's observation
-      // loads all in flight together; padding lanes and rows past B read zeros
-      const float *ob = obs + (size_t)step * B * P.in_dim;
-      const int nch = (P.in_pad + 63) >> 6;
-      for (int jb = wave; jb < GO2PI_TILE_ROWS * nch; jb += NW) {
-        const int r = jb / nch, c = jb - r * nch, row = row0 + r, k = c * 64 + lane;
-        const float *src = (row < B && k < P.in_dim) ? ob + (size_t)row * P.in_dim + k : P.zero + lane;
-        __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
-      }
-    } else {
-      const float *ob = obs + (size_t)step * B * P.in_dim;
-      for (int e = tid; e < GO2PI_TILE_ROWS * P.in_pad; e += NT) {
-        const int r = e / P.in_pad, k = e - r * P.in_pad, row = row0 + r;
-        float v = 0.f;
-        if (row < B && k < P.in_dim) v = prologue(P, ob[(size_t)row * P.in_dim + k], k);
-        bufA[r * S + k] = v;
-      }
-    }
-  };
-  // Step 0's observation loads go out first; their HBM latency overlaps the
-  // zero fill. Padded activation columns are read (against zero weights) by the
-  // next layer, so they must hold finite values: clear everything the
-  // observation does not cover, once.
-  stage_obs(0);
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
-#endif
-  if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int tail4 = (S - P.in_pad) >> 2;
-    for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
-      const int r = e / tail4;
-      reinterpret_cast<float4 *>(bufA + r * S + P.in_pad)[e - r * tail4] = z;
-    }
-    float4 *l4 = reinterpret_cast<float4 *>(bufB);
-    const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
-    for (int e = tid; e < n4; e += NT) l4[e] = z;
-  }
-  if (P.has_gru) {
-    __syncthreads();  // bufH zero fill above before the hidden rows land
-    if (W4T > 0 && H % 64 == 0) {
-      // pipeline: the hidden rows by direct-to-LDS loads, in flight with the
-      // observation's (one 64-column chunk per instruction; rows past B read zeros)
-      for (int i = 0; i < 4; ++i) {
-        const int r = wave + 4 * i, row = row0 + r;
-        for (int c = 0; c < (H >> 6); ++c) {
-          const float *src = row < B ? hidden + (size_t)row * H + c * 64 + lane : P.zero + lane;
-          __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufH + r * S + c * 64), 4, 0, 0);
-        }
-      }
-    } else {
-      for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-        const int r = e / H, k = e - r * H, row = row0 + r;
-        bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
-      }
-    }
-  }
-  for (int step = 0; step < steps; ++step) {
-    float *ac = act + (size_t)step * B * P.out_dim;
-    if (step > 0) stage_obs(step);
-    if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
-      static_assert(NW == 4, "one wave per SIMD");
-      float *X0 = bufA, *Y0 = bufB;
-      if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
-        auto carry = [&](auto gt_k) {  // (w4_gru waits for the x / h staging and barriers itself)  // the pipelined cell: h' to bufB, registers, and the carry
-          constexpr int GT = decltype(gt_k)::value;
-          float4 hn[GT];
-          w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
-                     P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr);
-          if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's hidden state: once, from registers
-            float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
-#pragma unroll
-            for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + i * 16) = hn[i];
-          }
-          __syncthreads();  // every wave has read bufH
-          float *hl = bufH + (lane & 15) * S + wave * GT * 16 + ((lane >> 4) << 2);
-#pragma unroll
-          for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hl + i * 16) = hn[i];
-        };
-        if (H == 256) {
-          carry(std::integral_constant<int, 4>{});
-        } else if (H == 128) {
-          carry(std::integral_constant<int, 2>{});
-        } else {
-          lds_dma_wait();
-          __syncthreads();  // x in bufA, the hidden rows in bufH
-          gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
-          __syncthreads();
-          for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-            const int r = e / H, k = e - r * H;
-            bufH[r * S + k] = bufB[r * S + k];  // read again only in the next step, after w4_step's barriers
-          }
-        }
-        X0 = bufB;
-        Y0 = bufA;
-#ifdef GO2PI_DIAG_GRUDBG
-        __syncthreads();
-        if (blockIdx.x == 0 && tid < 2)
-          printf("tid %d x %g %g %g h0 %g %g h1 %g %g %g S %d H %d in_pad %d has_gru %d\n", tid, bufA[tid * S],
-                 bufA[tid * S + 1], bufA[tid * S + 47], bufH[tid * S], bufH[tid * S + 255], bufB[tid * S],
-                 bufB[tid * S + 1], bufB[tid * S + 255], S, H, P.in_pad, P.has_gru);
-#endif
-      }
-      w4_step<W4T, W4H, CTL>(P, X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv, row0, B, ctl, CL,
-                             step);
-      continue;
-    }
-    lds_dma_wait();  // the observation tile's direct-to-LDS loads
-    __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-    if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
-#endif
-    if constexpr (CTL) {
-      if (ctl.status && tid < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + tid] = CL.nanf[tid];
-#ifdef GO2PI_DIAG_CLOCK
-      if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
-#endif
-    }
-    float *X = bufA, *Y = bufB;
-    if (P.has_gru) {
-      gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
-      __syncthreads();
-      for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-        const int r = e / H, k = e - r * H;
-        bufH[r * S + k] = bufB[r * S + k];
-      }
-      X = bufB;
-      Y = bufA;
-      // no barrier needed: layer 0 below reads bufB (X) and writes bufA (Y); bufH is
-      // next read after the end-of-step barrier
-    }
-    Handoff hin{nullptr, 0, 1};  // layer input complete: the barrier above
-    for (int l = 0; l < P.nl; ++l) {
-      const bool last = l == P.nl - 1;
-      if (P.head_fuse && l == P.nl - 2) {
-        if (P.head_fuse == 1)
-          dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
-        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
-        __syncthreads();
-        head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, cv, row0, B);
-#ifdef GO2PI_DIAG_CLOCK
-        if (tid == 0 && P.stamps && step == 0 && l < 8) {  // slots 6..14 (15 is the controller tick's)
-          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
-        }
-#endif
-        break;  // scratch is next written two barriers later; bufA/bufB are free
-      }
-      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B, hin);
-      // two wide layers in a row (both split by tiles over the waves, no split-K)
-      // hand off through per-wave flags instead of a workgroup barrier
-      const int T = P.L[l].N_pad >> 4;
-#ifdef GO2PI_DIAG_HANDOFF
-      // variant (diagnostics): flag hand-off between two wide layers. Measured
-      // slower than the barrier on MI355X (mlp512: 47.8 vs 45.6 us per launch;
-      // gru256: 78.4 vs 76.4 us), so the shipped build keeps the barrier.
-      const bool flag_next = !last && T >= NW && (P.L[l + 1].N_pad >> 4) >= NW;
-#else
-      const bool flag_next = false;  // a workgroup barrier after every layer
-#endif
-      if (flag_next) {
-        ++ep;
-        handoff_publish(flags, wave, lane, ep);
-        hin = Handoff{flags, ep, (T + NW - 1) / NW};
-        hin.err = P.err;
-      } else {
-        hin = Handoff{nullptr, 0, 1};
-#ifdef GO2PI_DIAG_PREFETCH  // variant (diagnostics): measured slower, see DESIGN §4.1
-        if (!last) prefetch_first<NW>(P.L[l + 1], wave, lane, hin);
-#endif
-        __syncthreads();
-      }
-#ifdef GO2PI_DIAG_CLOCK
-      if (tid == 0 && P.stamps && step == 0 && l < 9)  // slots 6..14 (15 is the controller tick's)
-        P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-#endif
-      float *t = X;
-      X = Y;
-      Y = t;
-    }
-  }
-  if (P.has_gru && !(W4T > 0 && (H == 256 || H == 128))) {  // (the pipelined cells store it from registers)
-    for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
-      const int r = e / H, k = e - r * H, row = row0 + r;
-      if (row < B) hidden[(size_t)row * H + k] = bufH[r * S + k];
-    }
-  }
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 2] = __builtin_amdgcn_s_memtime();
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 3] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
-}
-
-// W4T > 0: the 4-wave uniform-MLP pipeline with W4T tiles per wave and a W4H-tile
-// head (one kernel per shape: a single pipeline per kernel keeps the program
-// argument in SGPRs and the ring in registers)
-// The program is read from its device-memory copy (L2-resident across launches)
-// rather than passed by value: a by-value kernarg is a fresh copy per launch, and
-// every cache line of it a workgroup first touches is a memory round trip.
-template <int NW, int W4T = 0, int W4H = 0>
-__global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram *__restrict__ Pd,
-                                                               const float *__restrict__ obs,
-                                                               float *__restrict__ act, float *__restrict__ hidden,
-                                                               int B, int steps) {
-  fused_body<NW, false, W4T, W4H>(*Pd, obs, act, hidden, B, steps, DevCtl{});
-}
-
-template <int NW, int W4T = 0, int W4H = 0>
-__global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
-                                                                   float *__restrict__ hidden, int B) {
-  fused_body<NW, true, W4T, W4H>(*Pd, nullptr, nullptr, hidden, B, 1, C);
-}
 
 // ---------------------------------------------------------------------------
 // Small-batch GEMV layer. grid = N_pad/16 workgroups (one per 16-output tile),
@@ -1908,46 +355,46 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
   return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
 }
 
-static size_t fused_ctl_lds_bytes(const DevProgram &p, int waves) {
-  return fused_lds_bytes(p, waves) + sizeof(float) * ctl_lds_floats(GO2PI_TILE_ROWS, p.in_dim);
-}
-
-template <int NW, int W4T = 0, int W4H = 0>
+template <int NW>
 static hipError_t set_fused_lds(const DevProgram &p) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW, W4T, W4H>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds_bytes(p, NW));
   if (e != hipSuccess) return e;
   const size_t ctl = fused_ctl_lds_bytes(p, NW);
   if (ctl > 160 * 1024) return hipSuccess;  // controller tick unavailable for this width (launch fails loudly)
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW, W4T, W4H>),
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ctl);
 }
 
-// The kernel instantiation for (waves, p.w4_tpw, p.head_fuse): f(kernel tag).
-template <int NW, int W4T, int W4H>
+// The generic-body instantiation for `waves` (the 4-wave pipeline's live in
+// kernels_w4_t{2,4,8}.hip, one translation unit per tiles-per-wave: w4_*<TPW>).
+template <int NW>
 struct FusedTag {};
 template <class F>
-static void with_fused(const DevProgram &p, int waves, F &&f) {
-  if (waves == 4 && p.w4_tpw) {
-    const bool h2 = p.head_fuse == 2;
-    switch (p.w4_tpw) {
-      case 2: h2 ? f(FusedTag<4, 2, 2>{}) : f(FusedTag<4, 2, 1>{}); return;
-      case 4: h2 ? f(FusedTag<4, 4, 2>{}) : f(FusedTag<4, 4, 1>{}); return;
-      default: f(FusedTag<4, 8, 1>{}); return;  // 8 tiles per wave: one head tile only (engine.cpp)
-    }
-  }
+static void with_fused(int waves, F &&f) {
   switch (waves) {
-    case 4: f(FusedTag<4, 0, 0>{}); return;
-    case 16: f(FusedTag<16, 0, 0>{}); return;
-    default: f(FusedTag<8, 0, 0>{}); return;
+    case 4: f(FusedTag<4>{}); return;
+    case 16: f(FusedTag<16>{}); return;
+    default: f(FusedTag<8>{}); return;
+  }
+}
+
+template <class F>
+static int with_w4(const DevProgram &p, F &&f) {
+  switch (p.w4_tpw) {
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    default: return f(std::integral_constant<int, 8>{});
   }
 }
 
 int configure_kernels(const DevProgram &p, int waves) {
   hipError_t e = hipSuccess;
-  with_fused(p, waves, [&](auto tag) {
-    e = [&]<int NW, int T, int H>(FusedTag<NW, T, H>) { return set_fused_lds<NW, T, H>(p); }(tag);
-  });
+  if (waves == 4 && p.w4_tpw) {
+    e = (hipError_t)with_w4(p, [&](auto t) { return w4_configure<decltype(t)::value>(p); });
+  } else {
+    with_fused(waves, [&](auto tag) { e = [&]<int NW>(FusedTag<NW>) { return set_fused_lds<NW>(p); }(tag); });
+  }
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
   for (int l = 0; l < p.nl; ++l) gmax = std::max(gmax, (int)gemv_lds_bytes(p, l));
@@ -1959,13 +406,17 @@ int configure_kernels(const DevProgram &p, int waves) {
 int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves, const float *obs, float *act,
                         float *hidden, int batch, int steps, void *stream) {
   if (batch <= 0 || steps <= 0) return 0;
+  if (waves == 4 && p.w4_tpw)
+    return with_w4(p, [&](auto t) {
+      return w4_launch<decltype(t)::value>(p, p_dev, obs, act, hidden, batch, steps, stream);
+    });
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_lds_bytes(p, waves);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(p, waves, [&](auto tag) {
-    [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
-      hipLaunchKernelGGL((policy_fused_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p_dev, obs, act, hidden,
-                         batch, steps);
+  with_fused(waves, [&](auto tag) {
+    [&]<int NW>(FusedTag<NW>) {
+      hipLaunchKernelGGL((policy_fused_kernel<NW>), grid, dim3(NW * 64), lds, s, p_dev, obs, act, hidden, batch,
+                         steps);
     }(tag);
   });
   return (int)hipGetLastError();
@@ -1974,14 +425,15 @@ int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves,
 int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int waves, const DevCtl &ctl,
                             float *hidden, int batch, void *stream) {
   if (batch <= 0) return 0;
-  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_ctl_lds_bytes(p, waves);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (waves == 4 && p.w4_tpw)
+    return with_w4(p, [&](auto t) { return w4_launch_ctl<decltype(t)::value>(p, p_dev, ctl, hidden, batch, stream); });
+  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(p, waves, [&](auto tag) {
-    [&]<int NW, int T, int H>(FusedTag<NW, T, H>) {
-      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, T, H>), grid, dim3(NW * 64), lds, s, p_dev, ctl, hidden,
-                         batch);
+  with_fused(waves, [&](auto tag) {
+    [&]<int NW>(FusedTag<NW>) {
+      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW>), grid, dim3(NW * 64), lds, s, p_dev, ctl, hidden, batch);
     }(tag);
   });
   return (int)hipGetLastError();

@@ -42,6 +42,23 @@ struct DevGru {
 };
 
 struct DevProgram {
+  // ---- hot block (the first 80 bytes): every field the 4-wave pipeline reads,
+  // so that one scalar burst at kernel start fetches all of it (the fields'
+  // scattered lazy loads were a chain of ~7 dependent scalar round trips before
+  // the first observation load; fused_impl.hpp W4Hot). Set for pipeline programs.
+  const float *l0_w;       // = L[0].w, the base of the packed dense layers (back to back)
+  const float *head_w;     // = L[nl - 1].w
+  const float *head_bias;  // = L[nl - 1].bias
+  const float *bpack;      // = w4_bpack
+  const float *zero_hot;   // = zero
+  unsigned *err_hot;       // = err
+  int nbias;               // = w4_bias
+  int head_n;              // = L[nl - 1].N
+  int c0;                  // = L[0].K_pad / 16 (layer 0's k-chunks)
+  int in_dim_hot;          // = in_dim
+  int hid_act, head_act;   // activation of every hidden layer (uniform), of the head
+  float hid_alpha, head_alpha;
+  // ---- the rest
   int nl;
   int in_dim, in_pad, out_dim;
   int lds_stride;  // floats per row of an LDS activation buffer
@@ -51,6 +68,8 @@ struct DevProgram {
   int w4_tpw;      // >0: 4-wave uniform-MLP pipeline (kernels.hip, w4_step), tiles per wave of every hidden layer
   int w4_bias;     // pipeline: LDS floats holding every hidden layer's bias (sum of their N_pad), else 0
   const float *w4_bpack;  // pipeline: those biases packed back to back in device memory (one LDS-DMA stream)
+  int w4_plain;           // pipeline, 1: no prologue / epilogue arithmetic, no recurrent cell (the lean kernel)
+  int w4_c0m;             // pipeline: layer 0's k-chunks mod 4 (0 or 3; K padded to 16, not 64, when 3)
   // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
   const float *pre_sub;
   const float *pre_div;

@@ -157,7 +157,8 @@ template <int NF>
 __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (&w0)[NF], float b0, const float *obsv,
                                              float *x0, float *p0, float *xs, int B, int tid) {
   const DevLayer &L = P.L[0];
-  const int N0 = L.N_pad, K0 = L.K_pad, KS = (RES_WAVES * 64) / N0;
+  // x0 rows hold NF / 4 chunks per slice (zero-padded past layer 0's own chunks)
+  const int N0 = L.N_pad, KS = (RES_WAVES * 64) / N0, K0 = (NF / 4) * KS * 16;
   for (int i = tid; i < B * K0; i += RES_WAVES * 64) {
     const int b = i / K0, k = i - b * K0;
     x0[i] = k < P.in_dim ? prologue(P, obsv[b * P.in_dim + k], k) : 0.f;
@@ -217,7 +218,9 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   int *st = reinterpret_cast<int *>(part + RES_WAVES * GO2PI_SMALL_MAXB * 16);  // [0] leave, [1] epoch, [2] batch
   float *obsv = reinterpret_cast<float *>(st + 4);                   // [B][in_dim] the request's observation
   float *x0 = obsv + GO2PI_SMALL_MAXB * P.in_dim;                    // LOCAL0: [B][K0] prologued layer-0 input
-  float *p0 = x0 + GO2PI_SMALL_MAXB * P.L[0].K_pad;                  // LOCAL0, KS > 1: [KS][B][N0] partials
+  // LOCAL0: x0 rows of NF / 4 chunks per k-slice (>= K_pad), then the KS > 1 partials [KS][B][N0]
+  const int x0len = LOCAL0 ? (NF / 4) * ((RES_WAVES * 64) / P.L[0].N_pad) * 16 : P.L[0].K_pad;
+  float *p0 = x0 + GO2PI_SMALL_MAXB * x0len;
   // CTL: the LDS image of the tick's inputs (16-byte aligned: q0 is double)
   // (p0's size: KS * MAXB * N0 floats when 512 / N0 = KS > 1 slices, as launch_resident reserves)
   const int ks0 = ((RES_WAVES * 64) % P.L[0].N_pad == 0 && P.L[0].N_pad < RES_WAVES * 64) ? (RES_WAVES * 64) / P.L[0].N_pad : 0;
@@ -260,8 +263,9 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     const float4 *W = reinterpret_cast<const float4 *>(L.w);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const int c = ks + KS * (f >> 2), q = f & 3;
-      w0[f] = W[((size_t)c * (N0 >> 4) + (n >> 4)) * 64 + (n & 15) + 16 * q];
+      const int c = ks + KS * (f >> 2), q = f & 3;  // (chunks past layer 0's: zero fragments)
+      w0[f] = c < (L.K_pad >> 4) ? W[((size_t)c * (N0 >> 4) + (n >> 4)) * 64 + (n & 15) + 16 * q]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     b0 = L.bias[n];
   }
@@ -456,18 +460,20 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
   for (int l = 0; l < p.nl; ++l)
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
-  // local layer 0 where each thread's share of it fits NF = 8 or 16 registers' fragments
+  // local layer 0 where each thread's share of it fits NF = 8, 12 or 16 registers'
+  // fragments (a slice's chunks past layer 0's own are zero fragments on zero columns)
   const int N0 = p.L[0].N_pad, C0 = p.L[0].K_pad >> 4;
   const int KS = (N0 > 0 && (RES_WAVES * 64) % N0 == 0) ? (RES_WAVES * 64) / N0 : 0;
-  const int nf = (KS > 0 && C0 % KS == 0) ? 4 * (C0 / KS) : 0;
-  const bool local0 = p.nl >= 2 && (nf == 8 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
+  const int nf = KS > 0 ? 4 * ((C0 + KS - 1) / KS) : 0;
+  const bool local0 = p.nl >= 2 && (nf == 8 || nf == 12 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
+  const int x0len = local0 ? (nf / 4) * KS * 16 : p.L[0].K_pad;
   // one workgroup per 16-output tile of the widest TILED layer (with a local layer 0,
   // workgroups beyond the later layers' tiles would only repeat layer 0 and poll)
   int grid = 1;
   for (int l = local0 ? 1 : 0; l < p.nl; ++l) grid = std::max(grid, p.L[l].N_pad >> 4);
   // (the kernel's LDS carve-up: x0 and p0 are laid out whether used or not)
   const size_t ctl_off = ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
-                          (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * p.L[0].K_pad +
+                          (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * x0len +
                           (size_t)(KS > 1 ? KS : 0) * GO2PI_SMALL_MAXB * N0 + 3) / 4 * 4;
   const size_t lds =
       sizeof(float) * (ctl_off + (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) +
@@ -486,10 +492,12 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   };
   if (ctl) {
     if (local0 && nf == 8) return go(policy_resident_kernel<8, true>);
+    if (local0 && nf == 12) return go(policy_resident_kernel<12, true>);
     if (local0 && nf == 16) return go(policy_resident_kernel<16, true>);
     return go(policy_resident_kernel<0, true>);
   }
   if (local0 && nf == 8) return go(policy_resident_kernel<8, false>);
+  if (local0 && nf == 12) return go(policy_resident_kernel<12, false>);
   if (local0 && nf == 16) return go(policy_resident_kernel<16, false>);
   return go(policy_resident_kernel<0, false>);
 }
