@@ -14,6 +14,9 @@ Model specs:
   go2_gru_256 : observation[batch,48], h_in[1,batch,256] ->
                 Unsqueeze -> GRU(H=256, linear_before_reset=1) -> Squeeze ->
                 256->512^3->12 Elu head -> action[batch,12], h_out[1,batch,256]
+  go2_lstm_256: observation[batch,48], h_in, c_in[1,batch,256] ->
+                Unsqueeze -> LSTM(H=256) -> Squeeze -> 256->512^3->12 Elu head
+                -> action[batch,12], h_out, c_out[1,batch,256]
 """
 from __future__ import annotations
 
@@ -116,6 +119,48 @@ def gru_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch"
                     [("action", [batch, head[-1]]), ("h_out", [1, batch, H])])
 
 
+def lstm_params(I=48, H=256, seed=0):
+    bound = 1.0 / np.sqrt(H)
+    W = uniform(seed, 110, (1, 4 * H, I), bound)
+    R = uniform(seed, 111, (1, 4 * H, H), bound)
+    B = uniform(seed, 112, (1, 8 * H), bound)
+    return W, R, B
+
+
+def _head(cur, head, H, seed, nodes, inits):
+    layers = mlp_layers((H,) + tuple(head), seed, first_tid=200)
+    for i, (Wl, bl) in enumerate(layers):
+        wn, bn = f"head.{i}.weight", f"head.{i}.bias"
+        inits += [(wn, Wl), (bn, bl)]
+        last = i == len(layers) - 1
+        out = "action" if last else f"/head/{i}/Gemm_output_0"
+        nodes.append(ow.node("Gemm", [cur, wn, bn], [out], f"/head/{i}/Gemm",
+                             [ow.attr_float("alpha", 1.0), ow.attr_float("beta", 1.0), ow.attr_int("transB", 1)]))
+        cur = out
+        if not last:
+            aout = f"/head/{i}/Elu_output_0"
+            nodes.append(ow.node("Elu", [cur], [aout], f"/head/{i}/Elu", [ow.attr_float("alpha", 1.0)]))
+            cur = aout
+
+
+def lstm_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch") -> bytes:
+    """ONNX LSTM (gates i, o, f, c) as torch.onnx.export writes an nn.LSTM policy: the
+    observation unsqueezed to a 1-step sequence, (h, c) explicit graph I/O."""
+    W, R, B = lstm_params(I, H, seed)
+    axes = np.array([0], np.int64)
+    inits = [("lstm.W", W), ("lstm.R", R), ("lstm.B", B), ("axes0", axes)]
+    nodes = [
+        ow.node("Unsqueeze", ["observation", "axes0"], ["x_seq"], "/lstm/Unsqueeze"),
+        ow.node("LSTM", ["x_seq", "lstm.W", "lstm.R", "lstm.B", "", "h_in", "c_in"], ["lstm_Y", "h_out", "c_out"],
+                "/lstm/LSTM", [ow.attr_int("hidden_size", H)]),
+        ow.node("Squeeze", ["h_out", "axes0"], ["h_t"], "/lstm/Squeeze"),
+    ]
+    _head("h_t", head, H, seed, nodes, inits)
+    return ow.model(nodes, inits,
+                    [("observation", [batch, I]), ("h_in", [1, batch, H]), ("c_in", [1, batch, H])],
+                    [("action", [batch, head[-1]]), ("h_out", [1, batch, H]), ("c_out", [1, batch, H])])
+
+
 MODELS = {
     "go2_mlp_512": lambda: mlp_model_bytes(),
     "go2_gru_256": lambda: gru_model_bytes(),
@@ -135,6 +180,10 @@ MODELS = {
     "pipe_512_relu": lambda: mlp_model_bytes((70, 512, 512, 7), seed=12, act="Relu"),         # 8 x 1, K0 = 128
     "pipe_one_hidden": lambda: mlp_model_bytes((48, 256, 12), seed=13),                       # one hidden layer
     "gru_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=14),            # 2-tile GRU stage
+    # LSTM policies (the other recurrent cell of exported rsl_rl / Isaac policies)
+    "go2_lstm_256": lambda: lstm_model_bytes(),
+    "lstm_128": lambda: lstm_model_bytes(I=30, H=128, head=(256, 256, 12), seed=15),           # 2-tile LSTM stage
+    "lstm_small": lambda: lstm_model_bytes(I=10, H=32, head=(64, 6), seed=16),                 # generic body
 }
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

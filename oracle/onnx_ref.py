@@ -21,6 +21,12 @@ the reference's graph uses, evaluated on the reference's own weights
   linear_before_reset=1:  h~ = tanh(Wh x + Wbh + r * (Rh h + Rbh))
   linear_before_reset=0:  h~ = tanh(Wh x + Wbh + Rh (r * h) + Rbh)
   H' = (1 - z) * h~ + z * H.
+* `LSTM` (opset 14), the other recurrent cell exported policies use (SURVEY
+  §8f.3): gate order i, o, f, c; f = sigmoid, g = h = tanh; no peepholes,
+  input_forget = 0:
+  i = f(Wi x + Ri H + Wbi + Rbi), o = f(Wo x + Ro H + Wbo + Rbo),
+  f = f(Wf x + Rf H + Wbf + Rbf), c~ = g(Wc x + Rc H + Wbc + Rbc),
+  C' = f * C + i * c~, H' = o * h(C').
 
 The I/O contract mirrors `ONNXActor` (`onnx_inference/src/cpp/onnx_actor.cpp:23-35`):
 input 0 -> output 0, row-major float32, element count = shape[1].
@@ -295,6 +301,49 @@ def _gru(node: Node, env: dict, dt):
     return res
 
 
+def _lstm(node: Node, env: dict, dt):
+    """ONNX LSTM, layout=0, forward direction, no peepholes, one or more time steps."""
+    if int(node.attrs.get("input_forget", 0)) != 0:
+        raise NotImplementedError("oracle: LSTM input_forget=1")
+    if len(node.inputs) > 7 and node.inputs[7]:
+        raise NotImplementedError("oracle: LSTM peepholes")
+    X = env[node.inputs[0]].astype(dt)              # [T, B, I]
+    W = env[node.inputs[1]].astype(dt)[0]           # [4H, I]  (i, o, f, c)
+    R = env[node.inputs[2]].astype(dt)[0]           # [4H, H]
+    H = R.shape[1]
+    B = X.shape[1]
+    if len(node.inputs) > 3 and node.inputs[3]:
+        bias = env[node.inputs[3]].astype(dt)[0]    # [8H] = Wb(i,o,f,c) | Rb(i,o,f,c)
+    else:
+        bias = np.zeros(8 * H, dt)
+    h = np.zeros((B, H), dt)
+    c = np.zeros((B, H), dt)
+    if len(node.inputs) > 5 and node.inputs[5]:
+        h = env[node.inputs[5]].astype(dt)[0].copy()
+    if len(node.inputs) > 6 and node.inputs[6]:
+        c = env[node.inputs[6]].astype(dt)[0].copy()
+    b = bias[:4 * H] + bias[4 * H:]
+    Y = []
+    for t in range(X.shape[0]):
+        gates = X[t] @ W.T + h @ R.T + b             # [B, 4H]
+        i = _sigmoid(gates[:, :H])
+        o = _sigmoid(gates[:, H:2 * H])
+        f = _sigmoid(gates[:, 2 * H:3 * H])
+        cc = np.tanh(gates[:, 3 * H:])
+        c = f * c + i * cc
+        h = o * np.tanh(c)
+        Y.append(h)
+    outs = node.outputs
+    res = {}
+    if len(outs) > 0 and outs[0]:
+        res[outs[0]] = np.stack(Y)[:, None]          # [T, 1, B, H]
+    if len(outs) > 1 and outs[1]:
+        res[outs[1]] = h[None]                       # [1, B, H]
+    if len(outs) > 2 and outs[2]:
+        res[outs[2]] = c[None]
+    return res
+
+
 def run(g: Graph, feeds: dict, dtype=np.float64) -> dict:
     """Evaluate the graph in node order with numpy in `dtype` arithmetic."""
     dt = np.dtype(dtype)
@@ -342,6 +391,8 @@ def run(g: Graph, feeds: dict, dtype=np.float64) -> dict:
             out = {nd.outputs[0]: np.clip(ins[0], lo, hi)}
         elif op == "GRU":
             out = _gru(nd, env, dt)
+        elif op == "LSTM":
+            out = _lstm(nd, env, dt)
         elif op in ("Squeeze", "Unsqueeze", "Identity", "Flatten", "Reshape"):
             x = ins[0]
             if op == "Squeeze":
