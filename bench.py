@@ -54,6 +54,10 @@ WORKLOADS = {
                                  "configs[4]: Go2 GRU-256 + 512x3 head, batch 4096/GPU, 100 ticks per launch "
                                  "(hidden rows carried in LDS)"),
     "shipped_b4096": ("__shipped__", 4096, 1, "shipped model 98->128x3->12, batch 4096/GPU"),
+    "go2_lstm_256_b4096": ("go2_lstm_256", 4096, 1, "LSTM-256 + 512x3 head, batch 4096/GPU, one tick per launch"),
+    "go2_lstm_256_b4096_seq100": ("go2_lstm_256", 4096, 100,
+                                  "LSTM-256 + 512x3 head, batch 4096/GPU, 100 ticks per launch "
+                                  "(h in LDS, c in registers)"),
 }
 
 

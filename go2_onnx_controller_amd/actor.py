@@ -91,15 +91,26 @@ class InferenceSession:
         if in_name not in input_feed:
             raise ValueError(f"missing input '{in_name}'")
         x = np.asarray(input_feed[in_name], dtype=np.float32).reshape(-1, e.in_dim)
+        B = x.shape[0]
+        # recurrent state: GRU h [H]; LSTM h [H] | c [H] (the engine keeps both per robot)
+        parts = [n for n, _ in e.inputs[1:]]           # h_in (, c_in)
+        width = e.hidden_dim // max(1, len(parts)) if e.hidden_dim else 0
         if e.hidden_dim:
             # explicit recurrent I/O when the caller feeds/asks for it; otherwise engine-resident
-            h_name = e.inputs[1][0] if len(e.inputs) > 1 else None
-            if h_name and h_name in input_feed:
-                e.set_hidden(np.asarray(input_feed[h_name], np.float32).reshape(-1, e.hidden_dim))
+            fed = [n in input_feed for n in parts]
+            if any(fed):
+                cur = e.get_hidden(B).reshape(B, len(parts), width) if not all(fed) else \
+                    np.empty((B, len(parts), width), np.float32)
+                for k, n in enumerate(parts):
+                    if n in input_feed:
+                        cur[:, k] = np.asarray(input_feed[n], np.float32).reshape(B, width)
+                e.set_hidden(cur.reshape(B, e.hidden_dim))
         y = e.run(x)
         results = {e.outputs[0][0]: y}
         if e.hidden_dim and len(e.outputs) > 1:
-            results[e.outputs[1][0]] = e.get_hidden(x.shape[0]).reshape(1, x.shape[0], e.hidden_dim)
+            st = e.get_hidden(B).reshape(B, len(parts), width)
+            for k, (n, _) in enumerate(e.outputs[1:1 + len(parts)]):
+                results[n] = np.ascontiguousarray(st[:, k]).reshape(1, B, width)
         names = output_names or [n for n, _ in e.outputs]
         return [results[n] for n in names]
 

@@ -384,15 +384,16 @@ void pack_dense(const go2pi::Dense &d, bool last, std::vector<float> &w, std::ve
   std::copy(d.b.begin(), d.b.end(), b.begin());
 }
 
-// GRU fragments: [Ht][Cx + Ch][gate z,r,h][lane] float4 over the concatenated
-// [x (I_pad) | h (H)] axis; x chunks carry W, h chunks carry R.
+// Recurrent-cell fragments: [Cx + Ch][Ht][gate][lane] float4 over the concatenated
+// [x (I_pad) | h (H)] axis; x chunks carry W, h chunks carry R. G = 3 gates (GRU:
+// z, r, h) or 4 (LSTM: i, o, f, c), in ONNX row order.
 void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
   I_pad = ceil64(g.I);  // whole 4-chunk groups of x (the pipelined cell's ring runs on them)
-  const int H = g.H, Ht = H / 16, Cx = I_pad / 16, Ch = H / 16, Cc = Cx + Ch;
-  w.assign((size_t)Ht * Cc * 3 * 64 * 4, 0.f);
+  const int H = g.H, Ht = H / 16, Cx = I_pad / 16, Ch = H / 16, Cc = Cx + Ch, G = g.G;
+  w.assign((size_t)Ht * Cc * G * 64 * 4, 0.f);
   for (int t = 0; t < Ht; ++t)
     for (int c = 0; c < Cc; ++c)
-      for (int gate = 0; gate < 3; ++gate)
+      for (int gate = 0; gate < G; ++gate)
         for (int lane = 0; lane < 64; ++lane)
           for (int j = 0; j < 4; ++j) {
             const int unit = 16 * t + (lane & 15);
@@ -405,7 +406,7 @@ void pack_gru(const go2pi::Gru &g, std::vector<float> &w, int &I_pad) {
               const int k = 16 * (c - Cx) + 4 * (lane >> 4) + j;
               v = g.R[(size_t)row * H + k];
             }
-            w[((((size_t)c * Ht + t) * 3 + gate) * 64 + lane) * 4 + j] = v;
+            w[((((size_t)c * Ht + t) * G + gate) * 64 + lane) * 4 + j] = v;
           }
 }
 
@@ -462,8 +463,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   if ((int)m.layers.size() > GO2PI_MAX_LAYERS)
     throw ApiError("policy has more than " + std::to_string(GO2PI_MAX_LAYERS) + " dense layers", GO2PI_E_MODEL);
   if (m.has_gru) {
-    if (m.gru.lbr != 1) throw ApiError("GRU linear_before_reset=0 is not supported yet (export with lbr=1)", GO2PI_E_MODEL);
-    if (m.gru.H % 16) throw ApiError("GRU hidden size must be a multiple of 16", GO2PI_E_MODEL);
+    if (m.gru.cell == 0 && m.gru.lbr != 1)
+      throw ApiError("GRU linear_before_reset=0 is not supported yet (export with lbr=1)", GO2PI_E_MODEL);
+    if (m.gru.H % 16) throw ApiError("recurrent hidden size must be a multiple of 16", GO2PI_E_MODEL);
   }
 
   int ndev = 0;
@@ -526,13 +528,18 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     std::vector<float> w;
     int ip;
     pack_gru(m.gru, w, ip);
-    const int H = m.gru.H;
+    const int H = m.gru.H, G = m.gru.G;
     std::vector<float> bzr(2 * H), bh(2 * H);
-    for (int j = 0; j < H; ++j) {
-      bzr[j] = m.gru.Wb[j] + m.gru.Rb[j];
-      bzr[H + j] = m.gru.Wb[H + j] + m.gru.Rb[H + j];
-      bh[j] = m.gru.Wb[2 * H + j];
-      bh[H + j] = m.gru.Rb[2 * H + j];
+    if (m.gru.cell == 1) {  // LSTM: every gate's two biases summed (i, o, f, c)
+      bzr.resize(4 * H);
+      for (int j = 0; j < 4 * H; ++j) bzr[j] = m.gru.Wb[j] + m.gru.Rb[j];
+    } else {
+      for (int j = 0; j < H; ++j) {
+        bzr[j] = m.gru.Wb[j] + m.gru.Rb[j];
+        bzr[H + j] = m.gru.Wb[H + j] + m.gru.Rb[H + j];
+        bh[j] = m.gru.Wb[2 * H + j];
+        bh[H + j] = m.gru.Rb[2 * H + j];
+      }
     }
     p.has_gru = 1;
     p.gru.w = e.upload(w);
@@ -542,12 +549,15 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.gru.I_pad = ip;
     p.gru.H = H;
     p.gru.lbr = m.gru.lbr;
+    p.gru.cell = m.gru.cell;
+    p.gru.sw = m.gru.cell == 1 ? 2 * H : H;
     p.in_pad = ip;
     maxw = std::max({maxw, ip, H});
-    flops += 2.0 * 3 * H * ((double)m.gru.I + H);
-    wbytes += 4.0 * (3.0 * H * (m.gru.I + H) + 6.0 * H);
-    e.d_hidden = e.dalloc<float>((size_t)e.opts.max_batch * H);
-    hip_check(hipMemsetAsync(e.d_hidden, 0, (size_t)e.opts.max_batch * H * sizeof(float), e.stream), "hipMemsetAsync");
+    flops += 2.0 * G * H * ((double)m.gru.I + H);
+    wbytes += 4.0 * ((double)G * H * (m.gru.I + H) + 2.0 * G * H);
+    const size_t sw = (size_t)p.gru.sw;
+    e.d_hidden = e.dalloc<float>((size_t)e.opts.max_batch * sw);
+    hip_check(hipMemsetAsync(e.d_hidden, 0, (size_t)e.opts.max_batch * sw * sizeof(float), e.stream), "hipMemsetAsync");
   } else {
     p.in_pad = p.L[0].K_pad;
   }
@@ -704,7 +714,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
 
   e.cost.flops_per_row = flops;
   e.cost.weight_bytes = wbytes;
-  e.cost.io_bytes_per_row = 4.0 * (m.in_dim + m.out_dim) + (m.has_gru ? 8.0 * m.gru.H : 0.0);
+  e.cost.io_bytes_per_row = 4.0 * (m.in_dim + m.out_dim) + (m.has_gru ? 8.0 * p.gru.sw : 0.0);
   e.cost.n_layers = p.nl;
   e.cost.has_gru = p.has_gru;
 }
@@ -923,7 +933,7 @@ int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_
 int go2pi_hidden_dim(const go2pi_engine *e, int64_t *hd) {
   return guarded([&] {
     check_engine(e);
-    if (hd) *hd = e->model.has_gru ? e->model.gru.H : 0;
+    if (hd) *hd = e->model.has_gru ? e->prog.gru.sw : 0;  // LSTM: h | c
     return GO2PI_OK;
   });
 }
@@ -933,7 +943,7 @@ int go2pi_reset_hidden(go2pi_engine *e, const uint8_t *mask, int64_t batch) {
     check_engine(e);
     if (!e->model.has_gru) return GO2PI_OK;
     hip_check(hipSetDevice(e->device), "hipSetDevice");
-    const int H = e->model.gru.H;
+    const int H = e->prog.gru.sw;  // state floats per robot
     if (!mask) {
       hip_check(hipMemsetAsync(e->d_hidden, 0, sizeof(float) * (size_t)e->opts.max_batch * H, e->stream), "hipMemsetAsync");
     } else {
@@ -962,7 +972,7 @@ int go2pi_get_hidden(go2pi_engine *e, float *h, int64_t batch) {
     if (!h) throw ApiError("null hidden buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-    hip_check(hipMemcpy(h, e->d_hidden, sizeof(float) * (size_t)batch * e->model.gru.H, hipMemcpyDeviceToHost),
+    hip_check(hipMemcpy(h, e->d_hidden, sizeof(float) * (size_t)batch * e->prog.gru.sw, hipMemcpyDeviceToHost),
               "hipMemcpy D2H");
     return GO2PI_OK;
   });
@@ -976,7 +986,7 @@ int go2pi_set_hidden(go2pi_engine *e, const float *h, int64_t batch) {
     if (!h) throw ApiError("null hidden buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-    hip_check(hipMemcpy(e->d_hidden, h, sizeof(float) * (size_t)batch * e->model.gru.H, hipMemcpyHostToDevice),
+    hip_check(hipMemcpy(e->d_hidden, h, sizeof(float) * (size_t)batch * e->prog.gru.sw, hipMemcpyHostToDevice),
               "hipMemcpy H2D");
     return GO2PI_OK;
   });
@@ -1188,7 +1198,8 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4>
       std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d>", t, h, c0m);
     else
-      std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d>", e->waves, t, h, c0m);
+      std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d>", e->waves, t, h, c0m,
+                    (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0);
     return GO2PI_OK;
   });
 }
@@ -1237,7 +1248,8 @@ int go2pi_inspect_model(const char *path, char *buf, size_t cap) {
     }
     j += "],\"gru\":";
     if (m.has_gru)
-      j += "{\"I\":" + std::to_string(m.gru.I) + ",\"H\":" + std::to_string(m.gru.H) + ",\"lbr\":" +
+      j += "{\"cell\":\"" + std::string(m.gru.cell ? "LSTM" : "GRU") + "\",\"I\":" + std::to_string(m.gru.I) +
+           ",\"H\":" + std::to_string(m.gru.H) + ",\"lbr\":" +
            std::to_string(m.gru.lbr) + ",\"w_sum\":" + num(sum(m.gru.W)) + ",\"r_sum\":" + num(sum(m.gru.R)) +
            ",\"b_sum\":" + num(sum(m.gru.Wb) + sum(m.gru.Rb)) + "}";
     else

@@ -673,6 +673,88 @@ __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const 
   for (; t < t_end; ++t) gru_group<1>(G, X, Hs, Y, xs, t, lane);
 }
 
+// LSTM cell (ONNX semantics: gates i, o, f, c; f = sigmoid, g = h = tanh; no
+// peepholes) for one 16-robot tile, generic body (any wave count). X: LDS rows
+// holding x in [0, I_pad); Hs: LDS hidden rows (stride xs). h' goes to Y[:, 0:H]
+// (the caller copies it into Hs after a barrier, as for the GRU); the cell state c
+// is elementwise per (robot, unit), so the lane that owns a unit reads c from and
+// writes c' to the engine's state rows in HBM (hidden[row][H + j]) itself.
+template <int GT>
+__device__ __forceinline__ void lstm_group(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                           int t_first, int lane, float *hidden, int row0, int B) {
+  const int Cx = G.I_pad >> 4, Ch = G.H >> 4, Cc = Cx + Ch, H = G.H;
+  const int col = lane & 15, r0 = (lane >> 4) << 2;
+  f32x4 acc[4][GT];  // gates i, o, f, c
+  const WStream ws(G.w);
+  int vo[GT];  // per-lane byte offset of tile t_first + i's gate-i fragment in chunk 0 (gate g: + g KiB)
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float b = G.bzr[g * H + j];
+      acc[g][i] = f32x4{b, b, b, b};
+    }
+    vo[i] = ((t_first + i) * 4 * 64 + lane) * 16;
+  }
+  const int csb = Ch * 4 * 1024;  // bytes per chunk: [chunk][tile][gate][lane]
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
+  float4 cur[4][GT];
+#pragma unroll
+  for (int i = 0; i < GT; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) cur[g][i] = ws.ld(vo[i] + 1024 * g, 0);
+  for (int c = 0; c < Cc; ++c) {
+    const float4 a = c < Cx ? *reinterpret_cast<const float4 *>(xrow + c * 16)
+                            : *reinterpret_cast<const float4 *>(hrow + (c - Cx) * 16);
+    float4 nxt[4][GT];
+    const int cn = min(c + 1, Cc - 1);
+#pragma unroll
+    for (int i = 0; i < GT; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) nxt[g][i] = ws.ld(vo[i] + 1024 * g, cn * csb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < GT; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g][i] = mfma4(f4c(a, j), f4c(cur[g][i], j), acc[g][i]);
+#pragma unroll
+    for (int i = 0; i < GT; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cur[g][i] = nxt[g][i];
+  }
+  const int sw = G.sw;
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r0 + e, grow = row0 + row;
+      const float ig = sigmoid_fast(acc[0][i][e]), og = sigmoid_fast(acc[1][i][e]);
+      const float fg = sigmoid_fast(acc[2][i][e]);
+      const float cg = 2.f * sigmoid_fast(2.f * acc[3][i][e]) - 1.f;  // tanh, ~1e-7 abs
+      const float c_old = grow < B ? hidden[(size_t)grow * sw + H + j] : 0.f;
+      const float c_new = fg * c_old + ig * cg;
+      Y[row * xs + j] = og * (2.f * sigmoid_fast(2.f * c_new) - 1.f);
+      if (grow < B) hidden[(size_t)grow * sw + H + j] = c_new;
+    }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void lstm_cell(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                          int wave, int lane, float *hidden, int row0, int B) {
+  const int Ht = G.H >> 4;
+  const int tpw = (Ht + NW - 1) / NW;
+  int t = wave * tpw;
+  const int t_end = min(t + tpw, Ht);
+  constexpr int GM = NW >= 8 ? 1 : 2;  // VGPR budget per wave count (four gates)
+  for (; t + GM <= t_end; t += GM) lstm_group<GM>(G, X, Hs, Y, xs, t, lane, hidden, row0, B);
+  for (; t < t_end; ++t) lstm_group<1>(G, X, Hs, Y, xs, t, lane, hidden, row0, B);
+}
+
 // ---------------------------------------------------------------------------
 // Uniform-MLP pipeline at one wave per SIMD (4 waves per workgroup; the engine
 // selects it for policies whose hidden layers are all 64 * TPW wide, TPW = 2, 4
@@ -1016,6 +1098,112 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
 #ifdef GO2PI_DIAG_CLOCK
   if (st && wave == 0 && lane == 0) st[45] = __builtin_amdgcn_s_memtime();
 #endif
+}
+
+// LSTM cell as the pipeline's front stage (one wave per SIMD), the sibling of
+// w4_gru: wave w owns hidden tiles [w * GT, (w + 1) * GT) (H = 64 * GT) over the
+// concatenated [x | h] chunks, four gate fragments per (chunk, tile) streamed by
+// the same register ring (RD = 1, a load every 2 MFMAs), output-major
+// accumulators: lane l holds units 16t + 4(l >> 4) + e of robot l & 15. The cell
+// state c of exactly those units lives in the caller's registers (c, in / out):
+// it is elementwise, so no other wave ever needs it and across the ticks of a
+// sequence it never leaves the CU. h' goes to Y rows and to hn.
+template <int GT>
+__device__ __forceinline__ void w4_lstm(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
+                                        int lane, float4 (&hn)[GT], float4 (&c)[GT]) {
+  constexpr int NF = 4 * GT;  // gate fragments per chunk
+  constexpr int NM = 4 * NF;  // MFMAs per chunk
+  const int Cx = G.I_pad >> 4, Ch = G.H >> 4, H = G.H;
+  const int t0 = wave * GT, u0 = (lane >> 4) << 2;
+  const WStream ws(G.w);
+  const int csb = Ch * 4 * 1024;  // bytes per chunk (all tiles, four gates)
+  int vo[GT];
+#pragma unroll
+  for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 4 * 64 + lane) * 16;
+  float4 f[4][NF];
+  asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
+#pragma unroll
+  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, 0);
+  wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
+  f32x4 acc[4][GT];
+#pragma unroll
+  for (int i = 0; i < GT; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float *xrow = X + (lane & 15) * xs + u0;
+  const float *hrow = Hs + (lane & 15) * xs + u0;
+  float4 a[2];
+  a[0] = *reinterpret_cast<const float4 *>(xrow);
+  // chunk c (slot S = c & 3); NEXT: chunk c + 1 exists; NX: chunk c + 1 is an x chunk
+  auto chunk = [&](auto s_k, auto next_k, auto nx_k, int cc) {
+    constexpr int S = decltype(s_k)::value;
+    constexpr bool NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
+    if constexpr (NEXT) {
+      if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (cc + 1) * 16);
+      else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (cc + 1 - Cx) * 16);
+    }
+    const float4 b = a[S & 1];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int jk = m / NF, i = (m % NF) / 4, g = m % 4;
+      acc[g][i] = mfma4(f4c(f[S][i * 4 + g], jk), f4c(b, jk), acc[g][i]);
+      if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
+        const int q = m >> 1;
+        __builtin_amdgcn_sched_barrier(0);
+        f[(S + 1) & 3][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, (cc + 1) * csb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  int cc = 0;
+  for (; cc + 4 < Cx; cc += 4) {
+    chunk(I0{}, T_{}, T_{}, cc);
+    chunk(I1{}, T_{}, T_{}, cc + 1);
+    chunk(I2{}, T_{}, T_{}, cc + 2);
+    chunk(I3{}, T_{}, T_{}, cc + 3);
+  }
+  chunk(I0{}, T_{}, T_{}, cc);
+  chunk(I1{}, T_{}, T_{}, cc + 1);
+  chunk(I2{}, T_{}, T_{}, cc + 2);
+  chunk(I3{}, T_{}, F_{}, cc + 3);  // the next chunk is the first h chunk
+  for (cc = Cx; cc + 4 < Cx + Ch; cc += 4) {
+    chunk(I0{}, T_{}, F_{}, cc);
+    chunk(I1{}, T_{}, F_{}, cc + 1);
+    chunk(I2{}, T_{}, F_{}, cc + 2);
+    chunk(I3{}, T_{}, F_{}, cc + 3);
+  }
+  chunk(I0{}, T_{}, F_{}, cc);
+  chunk(I1{}, T_{}, F_{}, cc + 1);
+  chunk(I2{}, T_{}, F_{}, cc + 2);
+  chunk(I3{}, F_{}, F_{}, cc + 3);
+  float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t0 + i) * 16 + u0;
+    const float4 bi = *reinterpret_cast<const float4 *>(G.bzr + j);
+    const float4 bo = *reinterpret_cast<const float4 *>(G.bzr + H + j);
+    const float4 bf = *reinterpret_cast<const float4 *>(G.bzr + 2 * H + j);
+    const float4 bc = *reinterpret_cast<const float4 *>(G.bzr + 3 * H + j);
+    float o[4], cn[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float ig = sigmoid_fast(acc[0][i][e] + f4c(bi, e));
+      const float og = sigmoid_fast(acc[1][i][e] + f4c(bo, e));
+      const float fg = sigmoid_fast(acc[2][i][e] + f4c(bf, e));
+      const float cg = 2.f * sigmoid_fast(2.f * (acc[3][i][e] + f4c(bc, e))) - 1.f;  // tanh, ~1e-7 abs
+      cn[e] = fg * f4c(c[i], e) + ig * cg;
+      o[e] = og * (2.f * sigmoid_fast(2.f * cn[e]) - 1.f);
+    }
+    c[i] = make_float4(cn[0], cn[1], cn[2], cn[3]);
+    hn[i] = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4 *>(yrow + i * 16) = hn[i];
+  }
 }
 
 // Launch-critical values of the pipeline, read in ONE scalar burst from the
@@ -1369,7 +1557,9 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
 #endif
 }
 
-template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0>
+// RNN: the recurrent cell this instantiation runs when the program has one (0 GRU,
+// 1 LSTM; one kernel per cell keeps the other cell's registers out of it).
+template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
 __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
                                            float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
                                            const DevCtl ctl) {
@@ -1384,7 +1574,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
-  const int H = P.gru.H;
+  const int H = P.gru.H, SW = P.gru.sw;  // hidden width; state floats per robot (LSTM: h | c)
 #ifdef GO2PI_DIAG_PRIO  // variant: static priority for the second-dispatched half of the waves
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -1508,16 +1698,25 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       for (int i = 0; i < 4; ++i) {
         const int r = wave + 4 * i, row = row0 + r;
         for (int c = 0; c < (H >> 6); ++c) {
-          const float *src = row < B ? hidden + (size_t)row * H + c * 64 + lane : P.zero + lane;
+          const float *src = row < B ? hidden + (size_t)row * SW + c * 64 + lane : P.zero + lane;
           __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufH + r * S + c * 64), 4, 0, 0);
         }
       }
     } else {
       for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
         const int r = e / H, k = e - r * H, row = row0 + r;
-        bufH[r * S + k] = row < B ? hidden[(size_t)row * H + k] : 0.f;
+        bufH[r * S + k] = row < B ? hidden[(size_t)row * SW + k] : 0.f;
       }
     }
+  }
+  // LSTM, pipeline: this lane's cell-state units (w4_lstm) in registers for the whole sequence
+  float4 creg[4];
+  if (RNN == 1 && W4T > 0 && P.has_gru && (H == 256 || H == 128)) {
+    const int GT = H >> 6, row = row0 + (lane & 15);
+    const float *cg = hidden + (size_t)row * SW + H + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      creg[i] = (i < GT && row < B) ? *reinterpret_cast<const float4 *>(cg + i * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   for (int step = 0; step < steps; ++step) {
     float *ac = act + (size_t)step * B * P.out_dim;
@@ -1526,15 +1725,31 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       static_assert(NW == 4, "one wave per SIMD");
       float *X0 = bufA, *Y0 = bufB;
       if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
-        auto carry = [&](auto gt_k) {  // (w4_gru waits for the x / h staging and barriers itself)  // the pipelined cell: h' to bufB, registers, and the carry
+        // the pipelined cell (w4_gru / w4_lstm wait for the x / h staging and barrier
+        // themselves): h' to bufB, registers, and the carry
+        auto carry = [&](auto gt_k) {
           constexpr int GT = decltype(gt_k)::value;
           float4 hn[GT];
-          w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
-                     P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr);
-          if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's hidden state: once, from registers
-            float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
+          constexpr bool lstm = RNN == 1;
+          if constexpr (lstm) {
+            float4 cr[GT];
+#pragma unroll
+            for (int i = 0; i < GT; ++i) cr[i] = creg[i];
+            w4_lstm<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn, cr);
+#pragma unroll
+            for (int i = 0; i < GT; ++i) creg[i] = cr[i];
+          } else {
+            w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
+                       P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr);
+          }
+          if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's state: once, from registers
+            float *hg = hidden + (size_t)(row0 + (lane & 15)) * SW + wave * GT * 16 + ((lane >> 4) << 2);
 #pragma unroll
             for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + i * 16) = hn[i];
+            if constexpr (lstm) {
+#pragma unroll
+              for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + H + i * 16) = creg[i];
+            }
           }
           __syncthreads();  // every wave has read bufH
           float *hl = bufH + (lane & 15) * S + wave * GT * 16 + ((lane >> 4) << 2);
@@ -1548,7 +1763,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         } else {
           lds_dma_wait();
           __syncthreads();  // x in bufA, the hidden rows in bufH
-          gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
+          if constexpr (RNN == 1) lstm_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane, hidden, row0, B);
+          else gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
           __syncthreads();
           for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
             const int r = e / H, k = e - r * H;
@@ -1583,7 +1799,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     }
     float *X = bufA, *Y = bufB;
     if (P.has_gru) {
-      gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
+      if constexpr (RNN == 1) lstm_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane, hidden, row0, B);
+      else gru_cell<NW>(P.gru, bufA, bufH, bufB, S, wave, lane);
       __syncthreads();
       for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
         const int r = e / H, k = e - r * H;
@@ -1647,7 +1864,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   if (P.has_gru && !(W4T > 0 && (H == 256 || H == 128))) {  // (the pipelined cells store it from registers)
     for (int e = tid; e < GO2PI_TILE_ROWS * H; e += NT) {
       const int r = e / H, k = e - r * H, row = row0 + r;
-      if (row < B) hidden[(size_t)row * H + k] = bufH[r * S + k];
+      if (row < B) hidden[(size_t)row * SW + k] = bufH[r * S + k];
     }
   }
 #ifdef GO2PI_DIAG_CLOCK
@@ -1680,12 +1897,12 @@ template <int TPW>
 int w4_launch_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, float *hidden, int batch,
                   void *stream);
 
-template <int NW, int W4T = 0, int W4H = 0, int C0M = 0>
+template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram *__restrict__ Pd,
                                                                const float *__restrict__ obs,
                                                                float *__restrict__ act, float *__restrict__ hidden,
                                                                int B, int steps) {
-  fused_body<NW, false, W4T, W4H, C0M>(*Pd, obs, act, hidden, B, steps, DevCtl{});
+  fused_body<NW, false, W4T, W4H, C0M, RNN>(*Pd, obs, act, hidden, B, steps, DevCtl{});
 }
 
 // The lean pipeline kernel (w4_plain_body). Argument order = preload order: the
@@ -1700,10 +1917,10 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(const float *__restrict
   w4_plain_body<TPW, HT, C0M>(*Pd, obs, act, l0w, bpack, B, steps, dims);
 }
 
-template <int NW, int W4T = 0, int W4H = 0, int C0M = 0>
+template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
                                                                    float *__restrict__ hidden, int B) {
-  fused_body<NW, true, W4T, W4H, C0M>(*Pd, nullptr, nullptr, hidden, B, 1, C);
+  fused_body<NW, true, W4T, W4H, C0M, RNN>(*Pd, nullptr, nullptr, hidden, B, 1, C);
 }
 
 }  // namespace go2pi

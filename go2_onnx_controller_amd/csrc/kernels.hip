@@ -355,27 +355,29 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
   return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
 }
 
-template <int NW>
+template <int NW, int RNN>
 static hipError_t set_fused_lds(const DevProgram &p) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW, 0, 0, 0, RNN>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds_bytes(p, NW));
   if (e != hipSuccess) return e;
   const size_t ctl = fused_ctl_lds_bytes(p, NW);
   if (ctl > 160 * 1024) return hipSuccess;  // controller tick unavailable for this width (launch fails loudly)
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW>),
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW, 0, 0, 0, RNN>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ctl);
 }
 
 // The generic-body instantiation for `waves` (the 4-wave pipeline's live in
 // kernels_w4_t{2,4,8}.hip, one translation unit per tiles-per-wave: w4_*<TPW>).
-template <int NW>
+template <int NW, int RNN>
 struct FusedTag {};
+// RNN: the recurrent cell (0 none / GRU, 1 LSTM)
 template <class F>
-static void with_fused(int waves, F &&f) {
+static void with_fused(const DevProgram &p, int waves, F &&f) {
+  const bool lstm = p.has_gru && p.gru.cell == 1;
   switch (waves) {
-    case 4: f(FusedTag<4>{}); return;
-    case 16: f(FusedTag<16>{}); return;
-    default: f(FusedTag<8>{}); return;
+    case 4: lstm ? f(FusedTag<4, 1>{}) : f(FusedTag<4, 0>{}); return;
+    case 16: lstm ? f(FusedTag<16, 1>{}) : f(FusedTag<16, 0>{}); return;
+    default: lstm ? f(FusedTag<8, 1>{}) : f(FusedTag<8, 0>{}); return;
   }
 }
 
@@ -393,7 +395,9 @@ int configure_kernels(const DevProgram &p, int waves) {
   if (waves == 4 && p.w4_tpw) {
     e = (hipError_t)with_w4(p, [&](auto t) { return w4_configure<decltype(t)::value>(p); });
   } else {
-    with_fused(waves, [&](auto tag) { e = [&]<int NW>(FusedTag<NW>) { return set_fused_lds<NW>(p); }(tag); });
+    with_fused(p, waves, [&](auto tag) {
+      e = [&]<int NW, int RNN>(FusedTag<NW, RNN>) { return set_fused_lds<NW, RNN>(p); }(tag);
+    });
   }
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
@@ -413,10 +417,10 @@ int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves,
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   const size_t lds = fused_lds_bytes(p, waves);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(waves, [&](auto tag) {
-    [&]<int NW>(FusedTag<NW>) {
-      hipLaunchKernelGGL((policy_fused_kernel<NW>), grid, dim3(NW * 64), lds, s, p_dev, obs, act, hidden, batch,
-                         steps);
+  with_fused(p, waves, [&](auto tag) {
+    [&]<int NW, int RNN>(FusedTag<NW, RNN>) {
+      hipLaunchKernelGGL((policy_fused_kernel<NW, 0, 0, 0, RNN>), grid, dim3(NW * 64), lds, s, p_dev, obs, act,
+                         hidden, batch, steps);
     }(tag);
   });
   return (int)hipGetLastError();
@@ -431,9 +435,10 @@ int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int wa
     return with_w4(p, [&](auto t) { return w4_launch_ctl<decltype(t)::value>(p, p_dev, ctl, hidden, batch, stream); });
   const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(waves, [&](auto tag) {
-    [&]<int NW>(FusedTag<NW>) {
-      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW>), grid, dim3(NW * 64), lds, s, p_dev, ctl, hidden, batch);
+  with_fused(p, waves, [&](auto tag) {
+    [&]<int NW, int RNN>(FusedTag<NW, RNN>) {
+      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, 0, 0, 0, RNN>), grid, dim3(NW * 64), lds, s, p_dev, ctl,
+                         hidden, batch);
     }(tag);
   });
   return (int)hipGetLastError();

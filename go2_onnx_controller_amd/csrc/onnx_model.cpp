@@ -415,37 +415,46 @@ Model parse_onnx(const uint8_t *data, size_t n) {
     } else if (nd.op == "Identity" || nd.op == "Flatten") {
       // pass-through on [B, F]
     } else if (nd.op == "Unsqueeze") {
-      // must feed a GRU: X [1, B, I]
+      // must feed the recurrent cell: X [1, B, I]
       const std::string u = nd.out[0];
       auto ci = consumers.find(u);
-      if (ci == consumers.end() || ci->second.size() != 1 || nodes[ci->second[0]].op != "GRU")
-        fail("Unsqueeze is only supported in front of a GRU");
-    } else if (nd.op == "GRU") {
-      if (m.has_gru) fail("only one GRU layer is supported");
-      if (!m.layers.empty()) fail("GRU must be the first layer of the policy");
-      if (nd.iattr("layout", 0) != 0) fail("GRU layout=1 unsupported");
-      auto dir = nd.attrs.find("direction");
-      (void)dir;  // string attribute; only 'forward' is emitted by policy exporters
+      if (ci == consumers.end() || ci->second.size() != 1 ||
+          (nodes[ci->second[0]].op != "GRU" && nodes[ci->second[0]].op != "LSTM"))
+        fail("Unsqueeze is only supported in front of a GRU or LSTM");
+    } else if (nd.op == "GRU" || nd.op == "LSTM") {
+      // ONNX GRU (opset 14: gates z, r, h) or LSTM (opset 14: gates i, o, f, c), one
+      // forward direction, default activations, as torch.onnx.export writes nn.GRU / nn.LSTM
+      const bool lstm = nd.op == "LSTM";
+      const std::string op = nd.op;
+      if (m.has_gru) fail("only one recurrent layer is supported");
+      if (!m.layers.empty()) fail(op + " must be the first layer of the policy");
+      if (nd.iattr("layout", 0) != 0) fail(op + " layout=1 unsupported");
       const Tensor &W = init(nd.in.at(1));
       const Tensor &R = init(nd.in.at(2));
-      if (W.dims.size() != 3 || W.dims[0] != 1) fail("GRU: W must be [1, 3H, I] (one direction)");
       Gru g;
+      g.cell = lstm ? 1 : 0;
+      g.G = lstm ? 4 : 3;
+      if (W.dims.size() != 3 || W.dims[0] != 1)
+        fail(op + ": W must be [1, " + std::to_string(g.G) + "H, I] (one direction)");
       g.H = int(R.dims.at(2));
       g.I = int(W.dims[2]);
-      if (W.dims[1] != 3 * g.H || R.dims[1] != 3 * g.H) fail("GRU: gate dims mismatch");
-      g.lbr = int(nd.iattr("linear_before_reset", 0));
+      if (W.dims[1] != g.G * g.H || R.dims[1] != g.G * g.H) fail(op + ": gate dims mismatch");
+      g.lbr = lstm ? 0 : int(nd.iattr("linear_before_reset", 0));
       g.W = W.f;
       g.R = R.f;
-      g.Wb.assign(3 * g.H, 0.f);
-      g.Rb.assign(3 * g.H, 0.f);
+      g.Wb.assign((size_t)g.G * g.H, 0.f);
+      g.Rb.assign((size_t)g.G * g.H, 0.f);
       if (nd.in.size() > 3 && !nd.in[3].empty()) {
         const Tensor &B = init(nd.in[3]);
-        if (B.numel() != 6 * g.H) fail("GRU: B must be [1, 6H]");
-        std::copy(B.f.begin(), B.f.begin() + 3 * g.H, g.Wb.begin());
-        std::copy(B.f.begin() + 3 * g.H, B.f.end(), g.Rb.begin());
+        if (B.numel() != (int64_t)2 * g.G * g.H) fail(op + ": B must be [1, " + std::to_string(2 * g.G) + "H]");
+        std::copy(B.f.begin(), B.f.begin() + (long)g.G * g.H, g.Wb.begin());
+        std::copy(B.f.begin() + (long)g.G * g.H, B.f.end(), g.Rb.begin());
       }
-      if (nd.in.size() > 4 && !nd.in[4].empty()) fail("GRU: sequence_lens unsupported");
-      if (nd.attrs.count("activations")) fail("GRU: custom activations unsupported");
+      if (nd.in.size() > 4 && !nd.in[4].empty()) fail(op + ": sequence_lens unsupported");
+      if (nd.attrs.count("activations")) fail(op + ": custom activations unsupported");
+      if (nd.attrs.count("clip")) fail(op + ": cell clip unsupported");
+      if (lstm && nd.iattr("input_forget", 0) != 0) fail("LSTM: input_forget=1 unsupported");
+      if (lstm && nd.in.size() > 7 && !nd.in[7].empty()) fail("LSTM: peepholes (input P) unsupported");
       m.gru = std::move(g);
       m.has_gru = true;
       // follow Y_h (output 1) if consumed, else Y (output 0)
@@ -457,7 +466,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       pending_bias_ok = false;
       continue;
     } else if (nd.op == "Squeeze") {
-      if (!m.has_gru) fail("Squeeze is only supported after a GRU");
+      if (!m.has_gru) fail("Squeeze is only supported after a GRU or LSTM");
     } else {
       fail("unsupported operator '" + nd.op + "' (node '" + nd.name + "')");
     }
@@ -468,7 +477,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   if (m.layers.empty()) fail("policy has no linear layer");
   const int first_in = m.has_gru ? m.gru.I : m.layers[0].K;
   m.in_dim = first_in;
-  if (m.has_gru && m.layers[0].K != m.gru.H) fail("GRU hidden size does not match the first dense layer");
+  if (m.has_gru && m.layers[0].K != m.gru.H) fail("recurrent hidden size does not match the first dense layer");
   for (size_t l = 1; l < m.layers.size(); ++l)
     if (m.layers[l].K != m.layers[l - 1].N) fail("layer " + std::to_string(l) + " input dim mismatch");
   m.out_dim = m.layers.back().N;

@@ -24,12 +24,16 @@ struct Dense {
 };
 
 // ONNX GRU (opset 14), forward, layout 0, one layer; gates ordered z, r, h.
+// The recurrent cell in front of the dense head: ONNX GRU (gates z, r, h) or
+// LSTM (gates i, o, f, c; no peepholes). G = 3 or 4 gates.
 struct Gru {
+  int cell = 0;              // 0 GRU, 1 LSTM
+  int G = 3;                 // gates
   int I = 0, H = 0;
-  int lbr = 0;               // linear_before_reset
-  std::vector<float> W;      // [3H][I]
-  std::vector<float> R;      // [3H][H]
-  std::vector<float> Wb, Rb; // [3H] each
+  int lbr = 0;               // GRU linear_before_reset
+  std::vector<float> W;      // [G*H][I]
+  std::vector<float> R;      // [G*H][H]
+  std::vector<float> Wb, Rb; // [G*H] each
 };
 
 struct IoInfo {

@@ -34,11 +34,15 @@ struct DevLayer {
   int pad0, pad1, pad2;
 };
 
+// The recurrent cell in front of the dense head (ONNX GRU or LSTM; the field
+// names are the GRU's). State per robot in HBM: h [H] (GRU), h [H] | c [H] (LSTM).
 struct DevGru {
-  const float *w;    // packed [Ht][Cx + Ch][3 gates][64] float4
-  const float *bzr;  // [2H]: Wb_z + Rb_z | Wb_r + Rb_r
-  const float *bh;   // [2H]: Wb_h | Rb_h
+  const float *w;    // packed [Cx + Ch][Ht][G gates][64] float4 (chunk-major)
+  const float *bzr;  // GRU: [2H] Wb_z + Rb_z | Wb_r + Rb_r; LSTM: [4H] Wb + Rb, gates i, o, f, c
+  const float *bh;   // GRU: [2H] Wb_h | Rb_h; LSTM: unused
   int I, I_pad, H, lbr;
+  int cell;          // 0 GRU, 1 LSTM
+  int sw;            // state floats per robot: H (GRU), 2H (LSTM)
 };
 
 struct DevProgram {

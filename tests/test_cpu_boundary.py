@@ -211,3 +211,52 @@ def test_cmake_package_config(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     r = subprocess.run([cmake, "--build", str(build)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("name", ["lstm_small", "go2_lstm_256"])
+def test_loader_lstm(synth_path, name):
+    """The C++ loader's view of an ONNX LSTM policy (gates i, o, f, c; h and c graph I/O)
+    against the oracle's own protobuf decoder: dims, cell kind and weight checksums."""
+    from go2_onnx_controller_amd.engine import inspect_model
+    from oracle import onnx_ref
+    p = synth_path(name)
+    v = inspect_model(p)
+    g = onnx_ref.load(p)
+    lstm = next(n for n in g.nodes if n.op_type == "LSTM")
+    W, R, B = (g.inits[lstm.inputs[i]].astype(np.float64) for i in (1, 2, 3))
+    assert v["gru"]["cell"] == "LSTM"
+    assert v["gru"]["H"] == R.shape[2] and v["gru"]["I"] == W.shape[2] and 4 * R.shape[2] == W.shape[1]
+    assert v["gru"]["w_sum"] == pytest.approx(W.sum(), rel=1e-9)
+    assert v["gru"]["r_sum"] == pytest.approx(R.sum(), rel=1e-9)
+    assert v["gru"]["b_sum"] == pytest.approx(B.sum(), rel=1e-9)
+    assert [i["name"] for i in v["inputs"]] == ["observation", "h_in", "c_in"]
+    assert [o["name"] for o in v["outputs"]] == ["action", "h_out", "c_out"]
+    assert v["layers"][0]["K"] == R.shape[2]
+
+
+def test_loader_rejects_unsupported_lstm_forms(synth_path):
+    """LSTM peepholes / input_forget / cell clip are refused at load with a clear message."""
+    from go2_onnx_controller_amd import onnx_writer as ow
+    from go2_onnx_controller_amd.engine import Go2piError, inspect_model
+    import tempfile
+    H, I = 16, 4
+    rng = np.random.default_rng(0)
+    W = rng.standard_normal((1, 4 * H, I)).astype(np.float32)
+    R = rng.standard_normal((1, 4 * H, H)).astype(np.float32)
+    Wh = rng.standard_normal((3, H)).astype(np.float32)
+    for attrs, extra_in, msg in (([ow.attr_int("input_forget", 1)], [], "input_forget"),
+                                 ([ow.attr_float("clip", 3.0)], [], "clip"),
+                                 ([], ["lstm.P"], "peephole")):
+        inits = [("lstm.W", W), ("lstm.R", R), ("axes0", np.array([0], np.int64)), ("w", Wh),
+                 ("lstm.P", np.zeros((1, 3 * H), np.float32))]
+        ins = ["x_seq", "lstm.W", "lstm.R", "", "", "", ""] + extra_in
+        nodes = [ow.node("Unsqueeze", ["observation", "axes0"], ["x_seq"], "u"),
+                 ow.node("LSTM", ins, ["Y", "h_out"], "lstm", [ow.attr_int("hidden_size", H)] + attrs),
+                 ow.node("Squeeze", ["h_out", "axes0"], ["h"], "s"),
+                 ow.node("Gemm", ["h", "w"], ["action"], "g", [ow.attr_int("transB", 1)])]
+        data = ow.model(nodes, inits, [("observation", ["batch", I])], [("action", ["batch", 3])])
+        with tempfile.NamedTemporaryFile(suffix=".onnx") as fh:
+            fh.write(data)
+            fh.flush()
+            with pytest.raises(Go2piError, match=msg):
+                inspect_model(fh.name)

@@ -122,3 +122,73 @@ def test_gru_lbr0_oracle_semantics():
     np.testing.assert_allclose(h1, (1 - z) * n1 + z * h, atol=1e-12)
     np.testing.assert_allclose(h0, (1 - z) * n0 + z * h, atol=1e-12)
     assert np.abs(h1 - h0).max() > 1e-3
+
+
+def _torch_gate_reorder(M, order, H):
+    """ONNX gate blocks (rows of H) reordered into torch's order."""
+    return np.concatenate([M[g * H:(g + 1) * H] for g in order], axis=0)
+
+
+@pytest.mark.parametrize("name", ["lstm_small", "lstm_128"])
+def test_lstm_oracle_matches_torch_lstm(synth_path, name):
+    """Pin the oracle's ONNX LSTM against PyTorch's own nn.LSTM (an independent
+    implementation, present in this image): ONNX gates i, o, f, c are torch's
+    i, f, g, o reordered; biases b_ih / b_hh are ONNX Wb / Rb. 6 ticks, random
+    initial (h, c), fp64."""
+    import torch
+    from oracle import onnx_ref
+    g = onnx_ref.load(synth_path(name))
+    node = next(n for n in g.nodes if n.op_type == "LSTM")
+    W, R, Bb = (g.inits[node.inputs[i]].astype(np.float64)[0] for i in (1, 2, 3))
+    H, I = R.shape[1], W.shape[1]
+    order = [0, 2, 3, 1]  # torch i, f, g, o from ONNX i, o, f, c
+    lstm = torch.nn.LSTM(I, H).double()
+    with torch.no_grad():
+        lstm.weight_ih_l0.copy_(torch.from_numpy(_torch_gate_reorder(W, order, H)))
+        lstm.weight_hh_l0.copy_(torch.from_numpy(_torch_gate_reorder(R, order, H)))
+        lstm.bias_ih_l0.copy_(torch.from_numpy(_torch_gate_reorder(Bb[:4 * H], order, H)))
+        lstm.bias_hh_l0.copy_(torch.from_numpy(_torch_gate_reorder(Bb[4 * H:], order, H)))
+    rng = np.random.default_rng(8)
+    B, T = 5, 6
+    xs = rng.standard_normal((T, B, I))
+    h = rng.standard_normal((1, B, H))
+    c = rng.standard_normal((1, B, H))
+    with torch.no_grad():
+        y_t, (h_t, c_t) = lstm(torch.from_numpy(xs), (torch.from_numpy(h), torch.from_numpy(c)))
+    env = {"x_seq": xs, node.inputs[1]: g.inits[node.inputs[1]], node.inputs[2]: g.inits[node.inputs[2]],
+           node.inputs[3]: g.inits[node.inputs[3]], "h_in": h, "c_in": c}
+    res = onnx_ref._lstm(node, env, np.float64)
+    np.testing.assert_allclose(res[node.outputs[0]][:, 0], y_t.numpy(), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(res[node.outputs[1]], h_t.numpy(), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(res[node.outputs[2]], c_t.numpy(), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["gru_small", "gru_128"])
+def test_gru_oracle_matches_torch_gru(synth_path, name):
+    """Pin the oracle's ONNX GRU (linear_before_reset = 1) against PyTorch's nn.GRU,
+    whose n-gate formula is lbr = 1: ONNX gates z, r, h are torch's r, z, n
+    reordered. 6 ticks, random initial h, fp64."""
+    import torch
+    from oracle import onnx_ref
+    g = onnx_ref.load(synth_path(name))
+    node = next(n for n in g.nodes if n.op_type == "GRU")
+    W, R, Bb = (g.inits[node.inputs[i]].astype(np.float64)[0] for i in (1, 2, 3))
+    H, I = R.shape[1], W.shape[1]
+    order = [1, 0, 2]  # torch r, z, n from ONNX z, r, h
+    gru = torch.nn.GRU(I, H).double()
+    with torch.no_grad():
+        gru.weight_ih_l0.copy_(torch.from_numpy(_torch_gate_reorder(W, order, H)))
+        gru.weight_hh_l0.copy_(torch.from_numpy(_torch_gate_reorder(R, order, H)))
+        gru.bias_ih_l0.copy_(torch.from_numpy(_torch_gate_reorder(Bb[:3 * H], order, H)))
+        gru.bias_hh_l0.copy_(torch.from_numpy(_torch_gate_reorder(Bb[3 * H:], order, H)))
+    rng = np.random.default_rng(9)
+    B, T = 5, 6
+    xs = rng.standard_normal((T, B, I))
+    h = rng.standard_normal((1, B, H))
+    with torch.no_grad():
+        y_t, h_t = gru(torch.from_numpy(xs), torch.from_numpy(h))
+    env = {"x_seq": xs, node.inputs[1]: g.inits[node.inputs[1]], node.inputs[2]: g.inits[node.inputs[2]],
+           node.inputs[3]: g.inits[node.inputs[3]], "h_in": h}
+    res = onnx_ref._gru(node, env, np.float64)
+    np.testing.assert_allclose(res[node.outputs[0]][:, 0], y_t.numpy(), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(res[node.outputs[1]], h_t.numpy(), rtol=0, atol=1e-12)

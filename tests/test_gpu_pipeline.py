@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 # instantiation names: policy_mlp_kernel<tiles per wave, head tiles, layer-0 chunks mod 4> (the lean
-# body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4>
+# body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
+# recurrent cell (0 none / GRU, 1 LSTM)>
 # (a 33-, 40- or 48-wide observation is padded to 48 columns: 3 chunks; 70 to 128)
 SHAPES = {
     "pipe_512_relu": "policy_mlp_kernel<8, 1, 0>",
@@ -42,15 +43,15 @@ def test_pipeline_shapes(synth_path, name):
     x = np.random.default_rng(7).standard_normal((300, in_dim)).astype(np.float32)
     with Engine(p, max_batch=512, small_batch=-1) as e, Engine(p, max_batch=512, waves=8, small_batch=-1) as gen:
         assert e.batched_kernel == SHAPES[name]
-        assert gen.batched_kernel == "policy_fused_kernel<8, 0, 0, 0>"
+        assert gen.batched_kernel == "policy_fused_kernel<8, 0, 0, 0, 0>"
         for B in (1, 16, 17, 300):
             want = onnx_ref.act(g, x[:B])
             assert abs_err(e.run(x[:B]), want) <= TOL, (name, B)
             assert abs_err(gen.run(x[:B]), want) <= TOL, (name, B)
 
 
-@pytest.mark.parametrize("name,kernel", [("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0>"),
-                                         ("gru_128", "policy_fused_kernel<4, 4, 1, 0>")])
+@pytest.mark.parametrize("name,kernel", [("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0>"),
+                                         ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0>")])
 def test_pipeline_gru_ticks(synth_path, name, kernel):
     """GRU front stage + MLP pipeline over several ticks (hidden state carried by
     the engine), against the fp64 ONNX GRU oracle, actions and hidden state."""
@@ -72,12 +73,13 @@ def test_pipeline_gru_ticks(synth_path, name, kernel):
             assert abs_err(e.get_hidden(B), h[0]) <= TOL, t
 
 
-@pytest.mark.parametrize("env,kernel_tail", [({}, "policy_mlp_kernel 3>"),
-                                             ({"GO2PI_NO_PLAIN": "1"}, "policy_fused_kernel 3>"),
-                                             ({"GO2PI_K0_PAD64": "1"}, "policy_mlp_kernel 0>"),
-                                             ({"GO2PI_NO_PLAIN": "1", "GO2PI_K0_PAD64": "1"}, "policy_fused_kernel 0>")])
+@pytest.mark.parametrize("env,kname,tail", [({}, "policy_mlp_kernel", "3>"),
+                                            ({"GO2PI_NO_PLAIN": "1"}, "policy_fused_kernel", "3, 0>"),
+                                            ({"GO2PI_K0_PAD64": "1"}, "policy_mlp_kernel", "0>"),
+                                            ({"GO2PI_NO_PLAIN": "1", "GO2PI_K0_PAD64": "1"}, "policy_fused_kernel",
+                                             "0, 0>")])
 @pytest.mark.parametrize("name", ["go2_mlp_512", "pipe_128_tanh_h2", "pipe_256_h2"])
-def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, kernel_tail):
+def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, kname, tail):
     """The lean body (no prologue / epilogue) and the general one, each with layer 0
     padded to 3 chunks (48 columns) or 4 (64): all four against the fp64 oracle
     (the engine reads the GO2PI_* switches at create; A/B diagnostics)."""
@@ -89,7 +91,6 @@ def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, k
     g = onnx_ref.load(p)
     x = np.random.default_rng(11).standard_normal((4096, g.inputs[0][1][1])).astype(np.float32)
     with Engine(p, max_batch=4096, small_batch=-1) as e:
-        kname, tail = kernel_tail.split()
         assert e.batched_kernel.startswith(kname) and e.batched_kernel.endswith(tail), e.batched_kernel
         for B in (5, 16, 4096):
             assert abs_err(e.run(x[:B]), onnx_ref.act(g, x[:B])) <= TOL, (B, env)
