@@ -511,6 +511,16 @@ def main():
             p50, p99 = latency_b1(model_path, local)
             out["latency_b1_launch_p50_us"] = round(p50, 2)
             out["latency_b1_launch_p99_us"] = round(p99, 2)
+            # the recurrent policy (configs[4]'s GRU-256) at batch 1: the resident kernel's GRU
+            # form (hidden rows carried inside the live kernel), then one fused launch per call
+            from go2_onnx_controller_amd import synth as _synth
+            gru_path = _synth.ensure_model("go2_gru_256")
+            p50, p99 = latency_b1(gru_path, local, resident_ms=100)
+            out["latency_b1_gru_p50_us"] = round(p50, 2)
+            out["latency_b1_gru_p99_us"] = round(p99, 2)
+            p50, p99 = latency_b1(gru_path, local)
+            out["latency_b1_gru_launch_p50_us"] = round(p50, 2)
+            out["latency_b1_gru_launch_p99_us"] = round(p99, 2)
         if not args.no_gru and mname == "go2_mlp_512":
             out["gru256"] = gru_leg(local)
         if not args.no_ctl:

@@ -132,6 +132,8 @@ struct go2pi_engine {
   unsigned epoch = 1, last_epoch = 0;
   // resident batch <= SMALL_MAXB path (resident.hip, opts.resident_ms > 0)
   bool resident_ok = false, resident_live = false;
+  bool resident_ctl_ok = false;  // the controller-tick form applies (dense policies)
+  unsigned long long *d_hgran = nullptr;  // GRU form: [2][SMALL_MAXB][H] hidden-row granules (two buffers)
   bool resident_ctl = false;  // the live kernel is the controller-tick form
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
@@ -242,10 +244,14 @@ struct go2pi_engine {
     hip_check(hipMemsetAsync(d_mirror, 0, sizeof(unsigned long long) * (1 + GO2PI_SMALL_MAXB * (size_t)model.in_dim),
                              stream),
               "hipMemsetAsync");
+    if (d_hgran)
+      hip_check(hipMemsetAsync(d_hgran, 0, sizeof(unsigned long long) * 2 * GO2PI_SMALL_MAXB * (size_t)model.gru.H,
+                               stream),
+                "hipMemsetAsync");
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_act, d_gran, gstride, d_mirror, m_err, m_done,
-                                     res_idle_ticks, ctl, stream),
+                                     res_idle_ticks, ctl, d_hgran, d_hidden, stream),
               "resident launch");
     resident_live = true;
     resident_ctl = ctl != nullptr;
@@ -635,11 +641,16 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   {
     int kmax = 0;
     for (int l = 0; l < p.nl; ++l) kmax = std::max(kmax, p.L[l].K_pad);
-    e.latency_ok = !m.has_gru && kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
-                   !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
+    const bool lat_shape = kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
+                           !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
+    e.latency_ok = !m.has_gru && lat_shape;
+    // the resident kernel's GRU form (resident.hip, RNN): the cell tiled in front of
+    // the dense layers, h' carried between requests as granules
+    const bool res_rnn = m.has_gru && m.gru.cell == 0 && m.gru.lbr == 1 && m.gru.H % 64 == 0 &&
+                         p.gru.I_pad + m.gru.H <= 512 && (m.gru.H >> 4) <= 256 && lat_shape && e.opts.resident_ms > 0;
     e.palloc(&e.h_err, &e.m_err, 512);
     p.err = e.m_err + 64;  // batched kernel hand-off timeouts
-    if (e.latency_ok) {
+    if (e.latency_ok || res_rnn) {
       e.gstride = GO2PI_SMALL_MAXB * maxw;
       const size_t ng = (size_t)std::max(1, p.nl - 1) * e.gstride;
       e.d_gran = e.dalloc<unsigned long long>(ng);
@@ -648,8 +659,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       e.m_done = e.m_err + 32;
       e.done_ok = p.L[p.nl - 1].N_pad == 16;
     }
+    if (res_rnn && e.done_ok) e.d_hgran = e.dalloc<unsigned long long>(2 * (size_t)GO2PI_SMALL_MAXB * m.gru.H);
     // resident path: the latency kernel's program shape, the request ring in host memory
-    if (e.latency_ok && e.done_ok && e.opts.resident_ms > 0) {
+    if ((e.latency_ok || res_rnn) && e.done_ok && e.opts.resident_ms > 0) {
       // room for a controller tick's rows too (GO2PI_CTL_RAW + in_dim floats per robot)
       const size_t nreq = 1 + GO2PI_SMALL_MAXB * (size_t)(m.in_dim + GO2PI_CTL_RAW);
       e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
@@ -659,6 +671,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       if (khz <= 0) khz = 100000;
       e.res_idle_ticks = (unsigned long long)e.opts.resident_ms * (unsigned long long)khz;
       e.resident_ok = true;
+      e.resident_ctl_ok = !m.has_gru;  // the controller-tick form serves dense policies
     }
   }
   if (std::getenv("GO2PI_DIAG_STAMPS")) {  // diagnostics: per-workgroup clock stamps
@@ -1103,7 +1116,7 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
     c.kp = kp ? reinterpret_cast<double *>(dev + L.kp) : nullptr;
     c.kd = kd ? reinterpret_cast<double *>(dev + L.kd) : nullptr;
     c.status = status ? reinterpret_cast<uint32_t *>(dev + L.status) : nullptr;
-    const bool res = small && e->resident_ok && e->done_ok;
+    const bool res = small && e->resident_ok && e->resident_ctl_ok && e->done_ok;
     if (res) {
       // the resident kernel's controller form: every optional row has its place in the
       // staging; the header's flags say which this call passed

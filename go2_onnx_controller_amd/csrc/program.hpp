@@ -170,8 +170,13 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 #define GO2PI_RES_KP (1u << 10)
 #define GO2PI_RES_KD (1u << 11)
 #define GO2PI_RES_STATUS (1u << 12)
+// A GRU policy (p.has_gru, GRU lbr = 1, H % 64 == 0, ctl null) runs the cell as a
+// tiled layer: hgran = device [2][SMALL_MAXB][H] granules (zeroed before every
+// launch) carry h' between requests, hidden = the engine's state rows (read for
+// rows not yet written in this launch, written back when the kernel leaves).
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
-                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, void *stream);
+                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
+                    float *hidden, void *stream);
 
 }  // namespace go2pi

@@ -45,6 +45,7 @@ namespace {
 constexpr int RES_WAVES = 8;
 constexpr int RES_MAXS = 8;  // chunk slots per wave held in registers (K_pad <= 1024)
 constexpr int RES_POLL = 2;  // header + observation granules per lane in the idle poll (<= 127 obs floats)
+constexpr int RES_GS = 4;    // GRU form: gate-fragment chunk slots per wave (I_pad + H <= 512)
 
 typedef unsigned long long u64;
 
@@ -134,8 +135,12 @@ __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned 
   }
 }
 
-// Tag every granule this workgroup produces GO2PI_RES_LEAVE (all layers, all rows).
-__device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, int tid, int l0) {
+// Tag every granule this workgroup produces GO2PI_RES_LEAVE (all layers, all rows;
+// a GRU policy's hidden-row granules too).
+__device__ void tag_leave(const DevProgram &P, u64 *gran, int gstride, int g, int tid, int l0, u64 *hgran) {
+  if (hgran && g < (P.gru.H >> 4) && tid < 2 * GO2PI_SMALL_MAXB * 16)  // both buffers
+    __hip_atomic_store(hgran + (size_t)(tid >> 4) * P.gru.H + g * 16 + (tid & 15), (u64)GO2PI_RES_LEAVE << 32,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int l = l0; l + 1 < P.nl; ++l) {
     const DevLayer &L = P.L[l];
     if (g >= (L.N_pad >> 4)) continue;
@@ -205,11 +210,29 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
 // arrives, assembles the observation (ctl_fn.hpp, as policy_latency_ctl_kernel),
 // mirrors it, and post-processes the action into the staging (ctl_store); the
 // header's low word carries the batch and GO2PI_RES_* flags.
-template <int NF, bool CTL>
+//
+// RNN: a GRU policy (ONNX GRU, linear_before_reset = 1, H % 64 == 0). The cell
+// runs as a tiled layer in front of the dense ones: workgroup g < H / 16 owns
+// hidden units [16g, 16g + 16), its gate fragments held in registers for the
+// kernel's life; it computes z, r, n over [x | h] by GEMV (8 waves split the
+// k-chunks, fixed-order reductions) and publishes h' as {epoch, value} granules.
+// Those granules ARE the carried hidden state: dense layer 0 sweeps them as its
+// input (tag = this request's epoch), and the next request's cell sweeps them as
+// its h (tag = the epoch of the last request that covered that row). Every
+// workgroup tracks, per row, that epoch and which of two granule buffers
+// (hgran [2][8][H]) holds it, identically (all see the same requests): h' is
+// written to the OTHER buffer, because the request's other cell workgroups are
+// still reading the row's current h from this one (an in-place update raced
+// them). A row not yet written in this launch comes from the engine's state rows
+// in HBM; each cell workgroup writes its units' latest h' back to those rows when
+// the kernel leaves (not while it runs: the rows are read then).
+template <int NF, bool CTL, bool RNN = false>
 __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
                                                                          const u64 *req, float *act, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
-                                                                         unsigned *done, u64 idle_ticks, DevCtl C) {
+                                                                         unsigned *done, u64 idle_ticks, DevCtl C,
+                                                                         u64 *hgran, float *hidden) {
+  static_assert(!(RNN && (NF > 0 || CTL)), "the GRU form tiles layer 0 and serves act() only");
   constexpr bool LOCAL0 = NF > 0;
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
@@ -231,6 +254,37 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
   unsigned last = 0;
+  // RNN: the cell's LDS (after the CTL regions: RNN and CTL are exclusive)
+  const int Hh = RNN ? P.gru.H : 0, Ip = RNN ? P.gru.I_pad : 0, Kg = Ip + Hh, Cg = Kg >> 4, Cx = Ip >> 4;
+  const int Ht = Hh >> 4;
+  float *hx = cbase;                                      // [B][Kg] the cell's input rows [x | h]
+  float *hpart = hx + GO2PI_SMALL_MAXB * Kg;              // [waves][4][B][16] partial sums (z, r, n_x, n_h)
+  unsigned *le = reinterpret_cast<unsigned *>(hpart + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16);  // [B] row epochs
+  unsigned *lb = le + GO2PI_SMALL_MAXB;                   // [B] the granule buffer holding each row's h
+  float *hown = reinterpret_cast<float *>(lb + GO2PI_SMALL_MAXB);  // [B][16] this workgroup's units' latest h'
+  const size_t hbuf = (size_t)GO2PI_SMALL_MAXB * Hh;      // granules per buffer
+  float4 wgf[RES_GS][3];                                  // this workgroup's gate fragments (chunks wave + 8s)
+  float gb[4] = {0.f, 0.f, 0.f, 0.f};                     // its biases: z, r (summed), Wb_h, Rb_h
+  if constexpr (RNN) {
+    if (tid < GO2PI_SMALL_MAXB) le[tid] = lb[tid] = 0u;
+    if (g < Ht) {
+      const float4 *Wg = reinterpret_cast<const float4 *>(P.gru.w);
+#pragma unroll
+      for (int s = 0; s < RES_GS; ++s) {
+        const int c = wave + s * RES_WAVES;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          wgf[s][q] = c < Cg ? Wg[(((size_t)c * Ht + g) * 3 + q) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (wave == 0 && lane < 16) {
+        const int j = g * 16 + lane;
+        gb[0] = P.gru.bzr[j];
+        gb[1] = P.gru.bzr[Hh + j];
+        gb[2] = P.gru.bh[j];
+        gb[3] = P.gru.bh[Hh + j];
+      }
+    }
+  }
   // The weight fragments of the next layer this workgroup owns a tile of are
   // loaded one layer ahead, and those of its first layer before each request
   // wait, so a request meets them in registers (the launch-per-call kernel
@@ -342,6 +396,103 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       }
     }
 
+    // ---- RNN: the GRU cell (tiled; h' as granules tagged e, and to the state rows)
+    if constexpr (RNN) {
+      if (g < Ht) {
+        for (int i = tid; i < B * Ip; i += RES_WAVES * 64) {
+          const int b = i / Ip, k = i - b * Ip;
+          hx[b * Kg + k] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
+        }
+        if (wave < B) {  // wave b gathers row b's h: this launch's granules, else the state row
+          const int b = wave;
+          const unsigned te = le[b];
+          if (te != 0u) {
+            if (sweep<__HIP_MEMORY_SCOPE_AGENT>(hgran + lb[b] * hbuf + (size_t)b * Hh, Hh, te, hx + b * Kg + Ip, err,
+                                                lane) != 1 &&
+                lane == 0)
+              st[0] = 1;
+          } else {
+            for (int k = lane; k < Hh; k += 64) hx[b * Kg + Ip + k] = hidden[(size_t)b * Hh + k];
+          }
+        }
+        __syncthreads();
+        if (st[0]) left = true;
+#ifdef GO2PI_DIAG_RESDBG
+        if (tid == 0) printf("g %d e %u B %d gru staged left %d le0 %u hx %g %g\n", g, e, B, (int)left, le[0], hx[0], hx[Ip]);
+#endif
+        if (!left) {
+          float pz[GO2PI_SMALL_MAXB], pr[GO2PI_SMALL_MAXB], pnx[GO2PI_SMALL_MAXB], pnh[GO2PI_SMALL_MAXB];
+#pragma unroll
+          for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) pz[b] = pr[b] = pnx[b] = pnh[b] = 0.f;
+          const int koff = (lane >> 4) << 2;
+          auto dot4 = [](const float4 &a, const float4 &w, float acc) {
+            acc = fmaf(a.x, w.x, acc);
+            acc = fmaf(a.y, w.y, acc);
+            acc = fmaf(a.z, w.z, acc);
+            return fmaf(a.w, w.w, acc);
+          };
+#pragma unroll
+          for (int s = 0; s < RES_GS; ++s) {
+            const int c = wave + s * RES_WAVES;
+            if (c >= Cg) break;
+            const bool xc = c < Cx;
+#pragma unroll
+            for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+              if (b < B) {
+                const float4 a = *reinterpret_cast<const float4 *>(hx + b * Kg + c * 16 + koff);
+                pz[b] = dot4(a, wgf[s][0], pz[b]);
+                pr[b] = dot4(a, wgf[s][1], pr[b]);
+                if (xc) pnx[b] = dot4(a, wgf[s][2], pnx[b]);
+                else pnh[b] = dot4(a, wgf[s][2], pnh[b]);
+              }
+            }
+          }
+#pragma unroll
+          for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+            pz[b] += __shfl_xor(pz[b], 16);
+            pz[b] += __shfl_xor(pz[b], 32);
+            pr[b] += __shfl_xor(pr[b], 16);
+            pr[b] += __shfl_xor(pr[b], 32);
+            pnx[b] += __shfl_xor(pnx[b], 16);
+            pnx[b] += __shfl_xor(pnx[b], 32);
+            pnh[b] += __shfl_xor(pnh[b], 16);
+            pnh[b] += __shfl_xor(pnh[b], 32);
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
+              if (b < B) {
+                float *hp = hpart + ((size_t)wave * 4 * GO2PI_SMALL_MAXB + b) * 16 + lane;
+                hp[0] = pz[b];
+                hp[GO2PI_SMALL_MAXB * 16] = pr[b];
+                hp[2 * GO2PI_SMALL_MAXB * 16] = pnx[b];
+                hp[3 * GO2PI_SMALL_MAXB * 16] = pnh[b];
+              }
+            }
+          }
+          __syncthreads();
+          if (wave == 0 && lane < 16) {
+            const int j = g * 16 + lane;
+            for (int b = 0; b < B; ++b) {
+              float q[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                float a = 0.f;
+                for (int w2 = 0; w2 < RES_WAVES; ++w2) a += hpart[((w2 * 4 + k) * GO2PI_SMALL_MAXB + b) * 16 + lane];
+                q[k] = a + gb[k];
+              }
+              const float zg = sigmoid_fast(q[0]), rg = sigmoid_fast(q[1]);
+              const float hv = 2.f * sigmoid_fast(2.f * (q[2] + rg * q[3])) - 1.f;  // tanh, ~1e-7 abs
+              const float hnew = (1.f - zg) * hv + zg * hx[b * Kg + Ip + j];
+              hown[b * 16 + lane] = hnew;
+              __hip_atomic_store(hgran + (1u - lb[b]) * hbuf + (size_t)b * Hh + j, ((u64)e << 32) | __float_as_uint(hnew),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+        }
+      }
+      if (left) break;
+    }
     // ---- the layers (policy_latency_kernel's body; tags e + 1 + l)
     if constexpr (LOCAL0) local_layer0<NF>(P, w0, b0, obsv, x0, p0, xs, B, tid);
     for (int l = LOCAL0 ? 1 : 0; l < P.nl; ++l) {
@@ -349,7 +500,12 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
       if (g >= T) continue;  // this workgroup owns no tile of layer l
       // wr / bv hold layer l (prefetched)
-      if (l == 0) {
+      if (l == 0 && RNN) {  // the GRU's h' granules (tag e; row b in buffer 1 - lb[b]), [B][H] = [B][K_pad]
+        if (wave < B && sweep<__HIP_MEMORY_SCOPE_AGENT>(hgran + (1u - lb[wave]) * hbuf + (size_t)wave * Hh, Hh, e,
+                                                        xs + wave * K_pad, err, lane) != 1 &&
+            lane == 0)
+          st[0] = 1;
+      } else if (l == 0) {
         for (int i = tid; i < B * K_pad; i += RES_WAVES * 64) {
           const int b = i / K_pad, k = i - b * K_pad;
           xs[i] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
@@ -365,6 +521,9 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           st[0] = 1;
       }
       __syncthreads();
+#ifdef GO2PI_DIAG_RESDBG
+      if (tid == 0 && (g == 0 || g == 20)) printf("g %d e %u layer %d input ready st0 %d xs %g\n", g, e, l, st[0], xs[0]);
+#endif
       if (st[0]) {
         left = true;
         break;
@@ -433,6 +592,13 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       __syncthreads();  // xs / part reused by the next layer
     }
     if (left) break;
+    if constexpr (RNN) {  // rows [0, B) now carry this request's h' (granules tagged e, in the other buffer)
+      __syncthreads();     // every wave is done with lb for this request
+      if (tid < B) {
+        le[tid] = e;
+        lb[tid] = 1u - lb[tid];
+      }
+    }
     if constexpr (CTL) {
       if (g == 0) {  // the new observation rows and NaN flags, then the done word
         for (int i = tid; i < B * in_dim; i += RES_WAVES * 64) C.obs[i] = obsv[i];
@@ -445,7 +611,12 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     }
   }
   // ---- leave: consumers still waiting on this workgroup's slots leave too
-  tag_leave(P, gran, gstride, g, tid, LOCAL0 ? 1 : 0);
+  tag_leave(P, gran, gstride, g, tid, LOCAL0 ? 1 : 0, RNN ? hgran : nullptr);
+  if constexpr (RNN) {  // the rows this launch advanced go back to the engine's state rows
+    __syncthreads();
+    if (g < Ht && tid < GO2PI_SMALL_MAXB * 16 && le[tid >> 4] != 0u)
+      hidden[(size_t)(tid >> 4) * Hh + g * 16 + (tid & 15)] = hown[tid];
+  }
   if (g == 0 && tid == 0)
     __hip_atomic_store(mirror, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (g == 0 && tid == 0) {
@@ -456,29 +627,36 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
 
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
-                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, void *stream) {
+                    unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
+                    float *hidden, void *stream) {
   if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
   for (int l = 0; l < p.nl; ++l)
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
+  const bool rnn = p.has_gru != 0;
+  if (rnn && (ctl || p.gru.cell != 0 || p.gru.lbr != 1 || p.gru.H % 64 || p.gru.I_pad + p.gru.H > RES_GS * RES_WAVES * 16 ||
+              !hgran || !hidden))
+    return (int)hipErrorInvalidValue;
   // local layer 0 where each thread's share of it fits NF = 8, 12 or 16 registers'
   // fragments (a slice's chunks past layer 0's own are zero fragments on zero columns)
   const int N0 = p.L[0].N_pad, C0 = p.L[0].K_pad >> 4;
   const int KS = (N0 > 0 && (RES_WAVES * 64) % N0 == 0) ? (RES_WAVES * 64) / N0 : 0;
   const int nf = KS > 0 ? 4 * ((C0 + KS - 1) / KS) : 0;
-  const bool local0 = p.nl >= 2 && (nf == 8 || nf == 12 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
+  const bool local0 = !rnn && p.nl >= 2 && (nf == 8 || nf == 12 || nf == 16) && !std::getenv("GO2PI_RES_TILED0");
   const int x0len = local0 ? (nf / 4) * KS * 16 : p.L[0].K_pad;
   // one workgroup per 16-output tile of the widest TILED layer (with a local layer 0,
   // workgroups beyond the later layers' tiles would only repeat layer 0 and poll)
-  int grid = 1;
+  int grid = rnn ? (p.gru.H >> 4) : 1;
   for (int l = local0 ? 1 : 0; l < p.nl; ++l) grid = std::max(grid, p.L[l].N_pad >> 4);
   // (the kernel's LDS carve-up: x0 and p0 are laid out whether used or not)
   const size_t ctl_off = ((size_t)GO2PI_SMALL_MAXB * p.lds_stride + RES_WAVES * GO2PI_SMALL_MAXB * 16 + 4 +
                           (size_t)GO2PI_SMALL_MAXB * p.in_dim + (size_t)GO2PI_SMALL_MAXB * x0len +
                           (size_t)(KS > 1 ? KS : 0) * GO2PI_SMALL_MAXB * N0 + 3) / 4 * 4;
-  const size_t lds =
-      sizeof(float) * (ctl_off + (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) +
-                                            (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim)
-                                      : 0));
+  size_t tail = 0;
+  if (ctl) tail = (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
+  if (rnn)
+    tail = (size_t)GO2PI_SMALL_MAXB * (p.gru.I_pad + p.gru.H) + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16 +
+           2 * GO2PI_SMALL_MAXB + GO2PI_SMALL_MAXB * 16;
+  const size_t lds = sizeof(float) * (ctl_off + tail);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {
     if (lds > 64 * 1024) {
@@ -487,9 +665,10 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
       if (a != hipSuccess) return (int)a;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(RES_WAVES * 64), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req,
-                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{});
+                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden);
     return (int)hipGetLastError();
   };
+  if (rnn) return go(policy_resident_kernel<0, false, true>);
   if (ctl) {
     if (local0 && nf == 8) return go(policy_resident_kernel<8, true>);
     if (local0 && nf == 12) return go(policy_resident_kernel<12, true>);

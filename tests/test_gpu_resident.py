@@ -238,3 +238,65 @@ def test_entry_points_restore_current_device():
         e.sync()
         assert torch.cuda.current_device() == 0
     assert torch.cuda.current_device() == 0
+
+
+def _gru_oracle_step(path, x, h):
+    from oracle import onnx_ref
+    g = onnx_ref.load(path)
+    r = onnx_ref.run(g, {"observation": x.astype(np.float64), "h_in": h[None]})
+    return r["action"], r["h_out"][0]
+
+
+@pytest.mark.parametrize("name", ["go2_gru_256", "gru_128"])
+def test_resident_gru_rollout(synth_path, name):
+    """The resident kernel's GRU form (resident.hip, RNN): the hidden rows are carried
+    inside the live kernel between requests as tagged granules. 40 requests at batch
+    1..8 (rows past a request's batch keep their state), with a masked reset, a
+    set_hidden and get_hidden reads interleaved (each stops the kernel; the next
+    request relaunches and resumes from the engine's state rows), against the fp64
+    ONNX-GRU oracle rollout per row, and against the launch-per-call engine."""
+    from go2_onnx_controller_amd import Engine
+    p = synth_path(name)
+    rng = np.random.default_rng(17)
+    with Engine(p, max_batch=8, resident_ms=500) as r, Engine(p, max_batch=8) as q:
+        H = r.hidden_dim
+        h_ref = np.zeros((8, H))
+        r.reset_hidden()
+        q.reset_hidden()
+        for i in range(40):
+            B = [1, 1, 2, 8, 3, 1, 5, 8][i % 8]
+            x = rng.standard_normal((B, r.in_dim)).astype(np.float32)
+            want, h_new = _gru_oracle_step(p, x, h_ref[:B])
+            h_ref[:B] = h_new
+            y = r.run(x)
+            assert abs_err(y, want) <= TOL, f"request {i} B={B}"
+            assert abs_err(q.run(x), want) <= TOL, f"request {i} B={B} (launch path)"
+            if i == 12:  # masked reset (stops the kernel; the next request relaunches)
+                mask = np.array([1, 0, 1, 0, 0, 0, 0, 1], np.uint8)
+                r.reset_hidden(mask)
+                q.reset_hidden(mask)
+                h_ref[mask == 1] = 0
+            if i == 25:
+                s = rng.standard_normal((8, H)).astype(np.float32) * 0.5
+                r.set_hidden(s)
+                q.set_hidden(s)
+                h_ref[:] = s
+            if i % 10 == 9:
+                assert abs_err(r.get_hidden(8), h_ref) <= TOL, f"request {i}: hidden rows"
+
+
+def test_resident_gru_idle_exit_keeps_state(synth_path):
+    """resident_ms = 3: requests after pauses meet a kernel that has left (or is about
+    to); its h' stores to the state rows carry the hidden state across relaunches."""
+    from go2_onnx_controller_amd import Engine
+    p = synth_path("gru_128")
+    rng = np.random.default_rng(23)
+    with Engine(p, max_batch=8, resident_ms=3) as r:
+        h_ref = np.zeros((8, r.hidden_dim))
+        for i in range(30):
+            B = 1 + i % 3
+            x = rng.standard_normal((B, r.in_dim)).astype(np.float32)
+            want, h_new = _gru_oracle_step(p, x, h_ref[:B])
+            h_ref[:B] = h_new
+            assert abs_err(r.run(x), want) <= TOL, f"request {i}"
+            time.sleep(float(rng.uniform(0.0, 0.008)))
