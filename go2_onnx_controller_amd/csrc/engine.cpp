@@ -14,6 +14,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -99,6 +100,13 @@ struct DeviceRestore {
 
 }  // namespace
 
+namespace {
+void res_register(go2pi_engine *e);
+unsigned *yield_word(int device);
+void res_unregister(go2pi_engine *e);
+void evict_residents(const go2pi_engine *self);
+}  // namespace
+
 struct go2pi_engine {
   go2pi::Model model;
   go2pi_opts opts{};
@@ -132,6 +140,7 @@ struct go2pi_engine {
   unsigned epoch = 1, last_epoch = 0;
   // resident batch <= SMALL_MAXB path (resident.hip, opts.resident_ms > 0)
   bool resident_ok = false, resident_live = false;
+  std::atomic<int> res_flag{0};  // resident_live, readable from other threads (evict_residents)
   bool resident_ctl_ok = false;  // the controller-tick form applies (dense policies)
   unsigned long long *d_hgran = nullptr;  // GRU form: [2][SMALL_MAXB][H] hidden-row granules (two buffers)
   bool resident_ctl = false;  // the live kernel is the controller-tick form
@@ -152,6 +161,7 @@ struct go2pi_engine {
   // blocks go back to the process-wide cache).
   ~go2pi_engine() {
     DeviceRestore keep;
+    if (resident_ok) res_unregister(this);
     (void)hipSetDevice(device);
     if (resident_live) {  // tell the resident kernel to leave (the sync below waits for it)
       __atomic_store_n(h_req, (unsigned long long)GO2PI_RES_LEAVE << 32, __ATOMIC_SEQ_CST);
@@ -236,6 +246,7 @@ struct go2pi_engine {
     if (!resident_live) return;
     __atomic_store_n(h_req, (unsigned long long)GO2PI_RES_LEAVE << 32, __ATOMIC_SEQ_CST);
     resident_live = false;
+    res_flag.store(0);
     hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize (resident kernel leaving)");
   }
   void resident_start(const go2pi::DevCtl *ctl) {
@@ -251,9 +262,10 @@ struct go2pi_engine {
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_act, d_gran, gstride, d_mirror, m_err, m_done,
-                                     res_idle_ticks, ctl, d_hgran, d_hidden, stream),
+                                     res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
               "resident launch");
     resident_live = true;
+    res_flag.store(1);
     resident_ctl = ctl != nullptr;
     res_last = std::chrono::steady_clock::now();
   }
@@ -261,7 +273,10 @@ struct go2pi_engine {
   // the action lands in h_act. ctl: a controller tick, `rows` = its inputs concatenated
   // (state | joystick | obs | action, each batch rows); the outputs land in the staging
   // ctl names; flags = GO2PI_RES_* bits. The rows travel as tagged granules.
-  void resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
+  // false: not served because the kernel kept being told to leave (a batched launch
+  // on the device evicts live resident kernels, evict_residents): the caller serves
+  // the request by a launch instead; the kernel is relaunched by a later call.
+  bool resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
     if (resident_live && resident_ctl != (ctl != nullptr)) resident_stop();  // the other form is live
     const int n = (int)batch * (model.in_dim + (ctl ? GO2PI_CTL_RAW : 0));
     const auto idle = std::chrono::microseconds(1000LL * opts.resident_ms);  // (us: idle / 2 stays > 0 at 1 ms)
@@ -293,7 +308,7 @@ struct go2pi_engine {
         if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
       }
       res_last = std::chrono::steady_clock::now();
-      if (d == e0) return;
+      if (d == e0) return true;
       // the kernel left: wait for it to drain. An idle exit racing this request is
       // benign (serve it from a fresh launch with a fresh epoch); a hand-off timeout
       // (h_err set) is a device-side protocol fault and is reported, not retried
@@ -304,7 +319,7 @@ struct go2pi_engine {
       }
       if (d != GO2PI_RES_LEAVE)
         throw HipError("resident kernel did not answer within 2 s (request not served)", GO2PI_E_DEVICE);
-      if (attempt >= 1) throw HipError("resident kernel did not serve the request", GO2PI_E_DEVICE);
+      if (attempt >= 1) return false;  // evicted again (or idle exit twice): serve by a launch
     }
   }
 
@@ -370,6 +385,51 @@ struct go2pi_engine {
 };
 
 namespace {
+
+// Live resident kernels of every engine in the process, by device. A resident
+// kernel holds its workgroups' CUs while it waits for requests; a batched launch
+// (which wants all 256 CUs, one workgroup each) on the same device then runs in two
+// rounds: measured 37.8 -> 71.4 us per 4096-robot step (tools/interference.py,
+// DESIGN §4.2b). So every batched launch first tells the other engines' live
+// resident kernels on its device to leave (a LEAVE header; no wait), and their
+// next act() relaunches. GO2PI_RES_NO_EVICT=1 keeps them (A/B diagnostics).
+std::mutex g_res_mu;
+std::vector<go2pi_engine *> g_res_engines;
+
+void res_register(go2pi_engine *e) {
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  g_res_engines.push_back(e);
+}
+
+void res_unregister(go2pi_engine *e) {
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  g_res_engines.erase(std::remove(g_res_engines.begin(), g_res_engines.end(), e), g_res_engines.end());
+}
+
+// The batched-launch counter of each device (DevProgram::yield), one per process
+// and device, never freed (hipFree would synchronise the device).
+unsigned *yield_word(int device) {
+  static std::mutex mu;
+  static std::vector<unsigned *> words;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)words.size() <= device) words.resize(device + 1, nullptr);
+  if (!words[device]) {
+    void *p = nullptr;
+    hip_check(hipMalloc(&p, 256), "hipMalloc");
+    hip_check(hipMemset(p, 0, 256), "hipMemset");
+    words[device] = static_cast<unsigned *>(p);
+  }
+  return words[device];
+}
+
+void evict_residents(const go2pi_engine *self) {
+  static const bool off = std::getenv("GO2PI_RES_NO_EVICT") != nullptr;
+  if (off) return;
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  for (go2pi_engine *o : g_res_engines)
+    if (o != self && o->device == self->device && o->res_flag.load() == 1)
+      __atomic_store_n(o->h_req, (unsigned long long)GO2PI_RES_LEAVE << 32, __ATOMIC_SEQ_CST);
+}
 
 // K is padded to a multiple of 64 (4 chunks: the kernel's unroll); a hidden layer's
 // N to its consumer's K_pad (64), the final layer's N to 16 (one MFMA tile).
@@ -671,6 +731,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       if (khz <= 0) khz = 100000;
       e.res_idle_ticks = (unsigned long long)e.opts.resident_ms * (unsigned long long)khz;
       e.resident_ok = true;
+      res_register(&e);
       e.resident_ctl_ok = !m.has_gru;  // the controller-tick form serves dense policies
     }
   }
@@ -694,6 +755,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     go2pi_ctl_default_params(&cp);
     set_ctl_params(e, cp);
   }
+  p.yield = yield_word(e.device);
   // the pipeline's hot block (program.hpp): what it reads, in one scalar burst
   if (p.w4_tpw) {
     const auto &H = p.L[p.nl - 1];
@@ -874,13 +936,13 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
     if (batch == 0) return GO2PI_OK;
     if (!obs || !act) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
-    if (e->resident_ok && batch <= GO2PI_SMALL_MAXB) {
-      e->resident_serve(nullptr, obs, batch, 0u);
+    if (e->resident_ok && batch <= GO2PI_SMALL_MAXB && e->resident_serve(nullptr, obs, batch, 0u)) {
       e->check_handoff();
       std::memcpy(act, e->h_act, sizeof(float) * (size_t)batch * e->model.out_dim);
       return GO2PI_OK;
     }
     e->resident_stop();
+    if (batch > GO2PI_SMALL_MAXB || !e->latency_ok) evict_residents(e);  // a batched (fused) launch follows
     const size_t in_b = sizeof(float) * (size_t)batch * e->model.in_dim;
     const size_t out_b = sizeof(float) * (size_t)batch * e->model.out_dim;
     if (batch <= GO2PI_SMALL_MAXB) {
@@ -919,6 +981,7 @@ int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int6
     if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     e->check_handoff();  // a failure of an earlier asynchronous launch surfaces here (or at go2pi_sync)
+    if (!e->use_latency(batch)) evict_residents(e);
     e->enqueue(obs_dev, act_dev, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
   });
@@ -936,6 +999,7 @@ int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_
       throw ApiError("sequence too large", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    evict_residents(e);
     hip_check(go2pi::launch_policy_fused(e->prog, e->d_prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch,
                                          (int)steps, s),
               "fused sequence launch");
@@ -1117,6 +1181,7 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
     c.kd = kd ? reinterpret_cast<double *>(dev + L.kd) : nullptr;
     c.status = status ? reinterpret_cast<uint32_t *>(dev + L.status) : nullptr;
     const bool res = small && e->resident_ok && e->resident_ctl_ok && e->done_ok;
+    bool served = false;  // by the resident kernel
     if (res) {
       // the resident kernel's controller form: every optional row has its place in the
       // staging; the header's flags say which this call passed
@@ -1134,14 +1199,15 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
       else std::memset(rows + batch * GO2PI_CTL_STATE_DIM, 0, n_joy);
       std::memcpy(rows + batch * (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM), obs, n_obs);
       std::memcpy(rows + batch * (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM + in_dim), action, n_act);
-      e->resident_serve(&all, rows, batch, flags);
+      served = e->resident_serve(&all, rows, batch, flags);
     } else {
       e->resident_stop();
     }
-    const bool single = !res && small && e->use_latency(batch) && e->done_ok;
-    if (!res) e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
+    const bool single = !served && small && e->use_latency(batch) && e->done_ok;
+    if (!single && !served) evict_residents(e);  // a batched (fused) launch follows
+    if (!served) e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
     if (small) {
-      const bool synced = res || (single && e->spin_done());
+      const bool synced = served || (single && e->spin_done());
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
       e->check_handoff();
       std::memcpy(obs, e->h_ctl + L.obs, n_obs);
@@ -1177,6 +1243,7 @@ int go2pi_controller_step_device(go2pi_engine *e, const float *state, const floa
     // a live resident kernel shares the granules, epoch and error words the batch <= 8
     // launch uses: it leaves first (as for every other call on the engine)
     e->resident_stop();
+    if (!(e->use_latency(batch) && e->done_ok)) evict_residents(e);
     go2pi::DevCtl c{e->d_ctl, state, joy, obs, action, q_des, kp, kd, status};
     e->enqueue_ctl(c, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;

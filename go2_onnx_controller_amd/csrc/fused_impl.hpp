@@ -1509,9 +1509,11 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 template <int TPW, int HT, int C0M>
 __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *__restrict__ obs,
                                               float *__restrict__ act, const float *l0w, const float *bpack, int B,
-                                              int steps, unsigned dims) {
+                                              int steps, unsigned dims, unsigned *yield) {
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
+  // tell idle resident kernels on this device to give their CUs back (resident.hip)
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)(dims >> 20);
   // (the program's fields are read inside w4_step once the first loads are out)
   const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f};
@@ -1574,6 +1576,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
+  // tell idle resident kernels on this device to give their CUs back (resident.hip)
+  if (blockIdx.x == 0 && tid == 0 && P.yield)
+    __hip_atomic_fetch_add(P.yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int H = P.gru.H, SW = P.gru.sw;  // hidden width; state floats per robot (LSTM: h | c)
 #ifdef GO2PI_DIAG_PRIO  // variant: static priority for the second-dispatched half of the waves
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -1913,8 +1918,8 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(const float *__restrict
                                                          const float *__restrict__ l0w,
                                                          const float *__restrict__ bpack,
                                                          const DevProgram *__restrict__ Pd, int B, int steps,
-                                                         unsigned dims) {
-  w4_plain_body<TPW, HT, C0M>(*Pd, obs, act, l0w, bpack, B, steps, dims);
+                                                         unsigned dims, unsigned *yield) {
+  w4_plain_body<TPW, HT, C0M>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>

@@ -86,6 +86,9 @@ struct DevProgram {
   unsigned long long *stamps;  // diagnostics only (GO2PI_DIAG_CLOCK builds): 4 per workgroup
   const float *zero;           // >= 64 zero floats in device memory (source of the padding lanes' loads)
   unsigned *err;               // host-mapped word: set to 1 when a wave-to-wave layer hand-off times out
+  unsigned *yield;             // the device's batched-launch counter (one per device and process): every
+                               // batched kernel adds 1 at its start, an idle resident kernel that sees it
+                               // move leaves (it holds CUs the batched kernel needs; resident.hip)
   DevLayer L[GO2PI_MAX_LAYERS];
 };
 
@@ -170,6 +173,8 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 #define GO2PI_RES_KP (1u << 10)
 #define GO2PI_RES_KD (1u << 11)
 #define GO2PI_RES_STATUS (1u << 12)
+// yield: the device's batched-launch counter (DevProgram::yield): an idle resident
+// kernel leaves when a batched kernel starts.
 // A GRU policy (p.has_gru, GRU lbr = 1, H % 64 == 0, ctl null) runs the cell as a
 // tiled layer: hgran = device [2][SMALL_MAXB][H] granules (zeroed before every
 // launch) carry h' between requests, hidden = the engine's state rows (read for
@@ -177,6 +182,6 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
-                    float *hidden, void *stream);
+                    float *hidden, const unsigned *yield, void *stream);
 
 }  // namespace go2pi

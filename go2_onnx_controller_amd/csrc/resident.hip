@@ -88,14 +88,21 @@ __device__ __forceinline__ int sweep(const u64 *g, int n, unsigned tag, float *d
 // request is seen. Leaves (leave = 1) on a GO2PI_RES_LEAVE header or idle_ticks
 // of the 100 MHz wall clock without a request.
 template <int SCOPE, int NP = RES_POLL>
+// yield (workgroup 0 only, else null): the device's batched-launch counter (every
+// batched kernel adds 1 at its start); a change since y0 means a batched kernel
+// wants the CUs this kernel holds: leave (the next request relaunches).
 __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned last, u64 idle_ticks, float *obsv,
                                              unsigned *err, int lane, int &leave, unsigned &e, int &B,
-                                             unsigned &word) {
+                                             unsigned &word, const unsigned *yield = nullptr, unsigned y0 = 0) {
   u64 *qm = const_cast<u64 *>(q);
   const u64 t0 = wall_clock64();
   const int npoll = min(1 + in_dim, 64 * NP);
   leave = 0;
   for (;;) {
+    if (yield && __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != y0) {
+      leave = 1;
+      return;
+    }
     u64 v[NP];
 #pragma unroll
     for (int u = 0; u < NP; ++u)
@@ -231,7 +238,8 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
                                                                          const u64 *req, float *act, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
                                                                          unsigned *done, u64 idle_ticks, DevCtl C,
-                                                                         u64 *hgran, float *hidden) {
+                                                                         u64 *hgran, float *hidden,
+                                                                         const unsigned *yield) {
   static_assert(!(RNN && (NF > 0 || CTL)), "the GRU form tiles layer 0 and serves act() only");
   constexpr bool LOCAL0 = NF > 0;
   const DevProgram &P = *Pd;
@@ -254,6 +262,9 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
   unsigned last = 0;
+  // the batched-launch counter at launch (workgroup 0 leaves when it moves)
+  const unsigned y0 =
+      (g == 0 && yield) ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   // RNN: the cell's LDS (after the CTL regions: RNN and CTL are exclusive)
   const int Hh = RNN ? P.gru.H : 0, Ip = RNN ? P.gru.I_pad : 0, Kg = Ip + Hh, Cg = Kg >> 4, Cx = Ip >> 4;
   const int Ht = Hh >> 4;
@@ -337,9 +348,10 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         // one robot's 53 + in_dim floats arrive with the request); act: the observation
         if constexpr (CTL)
           wait_request<__HIP_MEMORY_SCOPE_SYSTEM, 3>(req, GO2PI_CTL_RAW + in_dim, last, idle_ticks, craw, err, lane,
-                                                     leave, e, B, word);
+                                                     leave, e, B, word, yield, y0);
         else
-          wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word);
+          wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
+                                                  yield, y0);
         const int n = (leave || CTL) ? 0 : B * in_dim;
         for (int i = lane; i < n; i += 64)
           __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
-                    float *hidden, void *stream) {
+                    float *hidden, const unsigned *yield, void *stream) {
   if (p.L[p.nl - 1].N_pad != 16) return (int)hipErrorInvalidValue;  // workgroup 0 owns the whole action
   for (int l = 0; l < p.nl; ++l)
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
@@ -665,7 +677,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
       if (a != hipSuccess) return (int)a;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(RES_WAVES * 64), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req,
-                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden);
+                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden, yield);
     return (int)hipGetLastError();
   };
   if (rnn) return go(policy_resident_kernel<0, false, true>);

@@ -300,3 +300,47 @@ def test_resident_gru_idle_exit_keeps_state(synth_path):
             h_ref[:B] = h_new
             assert abs_err(r.run(x), want) <= TOL, f"request {i}"
             time.sleep(float(rng.uniform(0.0, 0.008)))
+
+
+def test_batched_launch_evicts_other_resident_kernels(synth_path):
+    """A batched launch on the device tells other engines' live resident kernels to
+    leave (they hold CUs the launch needs: DESIGN §4.2b); the evicted engine's act()
+    keeps answering correctly from another thread throughout (a request met by the
+    eviction is served by a relaunch or by a launch), and the batched results stay
+    correct."""
+    import threading
+    import torch
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    pb = synth_path("go2_mlp_512")
+    ra, rb = mlp_ref.MlpRef.from_onnx(SHIPPED), mlp_ref.MlpRef.from_onnx(pb)
+    errs, n_act = [], [0]
+    stop = threading.Event()
+    with Engine(SHIPPED, max_batch=8, resident_ms=1000) as a, Engine(pb, max_batch=4096) as b:
+        x1 = realistic_obs(1, seed=3)
+        want1 = ra.f64(x1)
+
+        def tick():
+            try:
+                while not stop.is_set():
+                    if abs_err(a.run(x1), want1) > TOL:
+                        errs.append("act() output changed")
+                    n_act[0] += 1
+                    time.sleep(0.001)
+            except Exception as ex:  # noqa: BLE001 - reported below
+                errs.append(repr(ex))
+        th = threading.Thread(target=tick)
+        th.start()
+        try:
+            xb = torch.randn((4096, 48), device="cuda:0")
+            s = torch.cuda.Stream()
+            for _ in range(30):
+                yb = b.run_torch(xb, stream=s)
+                s.synchronize()
+                time.sleep(0.002)
+            assert abs_err(yb.cpu().numpy(), rb.f64(xb.cpu().numpy())) <= TOL
+        finally:
+            stop.set()
+            th.join(timeout=10)
+    assert not errs, errs
+    assert n_act[0] > 10
