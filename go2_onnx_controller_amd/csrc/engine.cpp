@@ -779,6 +779,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.w4_plain = !p.has_gru && !p.pre_sub && !p.pre_div && !(p.obs_clip > 0.f) && !p.post_tanh &&
                  std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) && p.clip_hi > 0 &&
                  p.scale == 1.f && p.lds_stride == 64 * p.w4_tpw + 4 && !std::getenv("GO2PI_NO_PLAIN");
+    // the lean kernel's compile-time activation: Elu (the exported rsl_rl / Isaac policies'), else runtime
+    p.w4_actc = (p.hid_act == 1 && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B diagnostics only
   }
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
@@ -1275,8 +1277,8 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
     const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
     const int c0m = t ? e->prog.w4_c0m : 0;
-    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4>
-      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d>", t, h, c0m);
+    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4, act>
+      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc);
     else
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0);

@@ -1225,6 +1225,19 @@ __device__ __forceinline__ W4Hot w4_hot(const DevProgram &P) {
                P.head_n,   P.c0,      P.hid_act,   P.head_act, P.hid_alpha, P.head_alpha};
 }
 
+// f(integral_constant<activation>): A >= 0 a compile-time activation (the lean
+// kernel's instantiation for the policy's one hidden activation: no dispatch, one
+// straight-line body the scheduler can interleave), A < 0 the runtime kind `act`.
+template <int A, class F>
+__device__ __forceinline__ void act_dispatch(int act, F &&f) {
+  if constexpr (A >= 0) {
+    (void)act;
+    f(std::integral_constant<int, A>{});
+  } else {
+    with_act(act, f);
+  }
+}
+
 // fragments of hidden layer l (l >= 1) of a TPW pipeline (arena layout above)
 template <int TPW>
 __device__ __forceinline__ const float *w4_layer_w(const W4Hot &h, int l) {
@@ -1239,7 +1252,7 @@ __device__ __forceinline__ const float *w4_layer_w(const W4Hot &h, int l) {
 // a 48- or 98-wide observation padded to 16 rather than 64): layer 0 starts on
 // ring slot (4 - C0M) & 3 so that its last chunk uses slot 3 and layer 1 starts on
 // slot 0 as always.
-template <int TPW, int HT, bool CTL, bool PL, int C0M>
+template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1>
 __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, float *X0, float *Y0, int S,
                                         f32x4 *scratch, int *flags, float *lbias, int &ep, int wave, int lane,
                                         float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
@@ -1364,7 +1377,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #ifdef GO2PI_DIAG_WEAVE
     // variant (diagnostics): layer l-1's epilogue of tile i+1 woven between layer l's
     // MFMAs of chunk t0+i (measured slower: the woven VALU stretches the MFMA gaps)
-    with_act(hot.hid_act, [&](auto act_k) {
+    act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
       float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
       *reinterpret_cast<float4 *>(yrow) = v;
@@ -1389,7 +1402,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
     // publish, then layer l's MFMAs over those chunks with the B operand from registers
     // (!HO: the epilogue to LDS, then a workgroup barrier)
-    with_act(hot.hid_act, [&](auto act_k) {
+    act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
       float4 v[TPW];
 #pragma unroll
@@ -1440,29 +1453,42 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     }
 #endif
   }
-  // the last hidden layer's epilogue feeds the head from registers (no LDS copy);
-  // two accumulator chains per head tile (even / odd k-tiles), summed in a fixed order
+  // the last hidden layer's epilogue feeds the head from registers (no LDS copy).
+  // Four accumulator chains per head tile, one per k-step of a chunk, so that no
+  // MFMA waits on the one before it (a single chain paid the dependent-accumulator
+  // latency 4 x TPW times), summed in a fixed order: (c0 + c1) + (c2 + c3).
   {
-    f32x4 hacc[HT][2];
+#ifdef GO2PI_DIAG_HEAD2  // variant (diagnostics): two chains (even / odd tiles)
+    constexpr int NCH = 2;
+#else
+    constexpr int NCH = 4;
+#endif
+    f32x4 hacc[HT][NCH];
 #pragma unroll
-    for (int h = 0; h < HT; ++h) hacc[h][0] = hacc[h][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    with_act(hot.hid_act, [&](auto act_k) {
+    for (int h = 0; h < HT; ++h)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) hacc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         const float4 v = w4_epi<ACT>(alpha, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
-          f32x4 &a = hacc[h][i & 1];
-          a = mfma4(hw[h][i].x, v.x, a);
-          a = mfma4(hw[h][i].y, v.y, a);
-          a = mfma4(hw[h][i].z, v.z, a);
-          a = mfma4(hw[h][i].w, v.w, a);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f32x4 &a = hacc[h][NCH == 4 ? j : (i & 1)];
+            a = mfma4(f4c(hw[h][i], j), f4c(v, j), a);
+          }
         }
       }
     });
 #pragma unroll
-    for (int h = 0; h < HT; ++h) scratch[(h * 4 + wave) * 64 + lane] = hacc[h][0] + hacc[h][1];
+    for (int h = 0; h < HT; ++h) {
+      f32x4 t = hacc[h][0] + hacc[h][1];
+      if constexpr (NCH == 4) t = t + (hacc[h][2] + hacc[h][3]);
+      scratch[(h * 4 + wave) * 64 + lane] = t;
+    }
   }
   __syncthreads();
 #ifdef GO2PI_DIAG_CLOCK
@@ -1506,7 +1532,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 // dims = in_dim | c0 << 12 | hidden layers << 20. The LDS stride is a
 // compile-time constant; padding lanes of the observation tile read an element of
 // the same row (times a zero weight column), rows past B the last row.
-template <int TPW, int HT, int C0M>
+template <int TPW, int HT, int C0M, int ACTC>
 __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *__restrict__ obs,
                                               float *__restrict__ act, const float *l0w, const float *bpack, int B,
                                               int steps, unsigned dims, unsigned *yield) {
@@ -1548,7 +1574,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
       P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    w4_step<TPW, HT, false, true, C0M>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
+    w4_step<TPW, HT, false, true, C0M, ACTC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
                                        CtlLds{}, step);
   }
 #ifdef GO2PI_DIAG_CLOCK
@@ -1913,13 +1939,13 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram 
 // The lean pipeline kernel (w4_plain_body). Argument order = preload order: the
 // first 16 dwords of the kernel arguments arrive in SGPRs (kernels_w4_t*.hip are
 // built with -amdgpu-kernarg-preload-count=16); these are 13.
-template <int TPW, int HT, int C0M>
+template <int TPW, int HT, int C0M, int ACTC>
 __global__ __launch_bounds__(256) void policy_mlp_kernel(const float *__restrict__ obs, float *__restrict__ act,
                                                          const float *__restrict__ l0w,
                                                          const float *__restrict__ bpack,
                                                          const DevProgram *__restrict__ Pd, int B, int steps,
                                                          unsigned dims, unsigned *yield) {
-  w4_plain_body<TPW, HT, C0M>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
+  w4_plain_body<TPW, HT, C0M, ACTC>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>

@@ -74,6 +74,7 @@ struct DevProgram {
   const float *w4_bpack;  // pipeline: those biases packed back to back in device memory (one LDS-DMA stream)
   int w4_plain;           // pipeline, 1: no prologue / epilogue arithmetic, no recurrent cell (the lean kernel)
   int w4_c0m;             // pipeline: layer 0's k-chunks mod 4 (0 or 3; K padded to 16, not 64, when 3)
+  int w4_actc;            // lean kernel: the hidden activation as a compile-time constant (1 = Elu), or -1
   // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
   const float *pre_sub;
   const float *pre_div;
