@@ -198,6 +198,9 @@ def gru_leg(device, launches=20, seq_ticks=100):
                         "frac_fp32_peak": round(tf / PEAK_FP32_TFLOPS, 4), "hidden_residency": res}
         out["kernel"] = e.batched_kernel
         out["robots"] = B
+        # memory-side bytes of one 100-tick launch (committed rocprofv3 FETCH/WRITE passes)
+        tr = load_pmc("go2_gru_256_b4096_seq100", e.batched_kernel)
+        out["seq100"]["traffic_bytes_per_launch"] = round(tr) if tr else None
     return out
 
 
