@@ -781,6 +781,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
                  p.scale == 1.f && p.lds_stride == 64 * p.w4_tpw + 4 && !std::getenv("GO2PI_NO_PLAIN");
     // the lean kernel's compile-time activation: Elu (the exported rsl_rl / Isaac policies'), else runtime
     p.w4_actc = (p.hid_act == 1 && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B diagnostics only
+    // ... and its hidden-layer count (3: the usual policy depth): the layer loop fully
+    // unrolled, so no ring-register copies (and no vmcnt(0)) at the layer boundaries
+    p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
   }
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
@@ -1277,8 +1280,9 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
     const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
     const int c0m = t ? e->prog.w4_c0m : 0;
-    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4, act>
-      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc);
+    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
+                                // act, hidden layers>
+      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
     else
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0);

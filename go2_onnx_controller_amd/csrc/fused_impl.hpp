@@ -896,7 +896,10 @@ __device__ __forceinline__ void w4_own_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][T
     (([&] {
        constexpr int J = M / TPW, I = M % TPW;
        acc[I] = mfma4(f4c(f[S][I], J), f4c(b, J), acc[I]);
-       if constexpr ((M & 3) == 3) f[(S + RD) & 3][M >> 2] = ws.ld(vo[M >> 2], soff);
+       // the next chunk's fragments as in w4_chunk: one load every LSP MFMAs from the
+       // chunk's start (every 4 left the last ones only 8 MFMAs ahead of their use)
+       constexpr int LSP = GO2PI_W4_LSP;
+       if constexpr (M % LSP == LSP - 1 && M / LSP < TPW) f[(S + RD) & 3][M / LSP] = ws.ld(vo[M / LSP], soff);
        stages_after(std::integral_constant<int, M>{});
        __builtin_amdgcn_sched_barrier(0);
      }()),
@@ -1252,7 +1255,7 @@ __device__ __forceinline__ const float *w4_layer_w(const W4Hot &h, int l) {
 // a 48- or 98-wide observation padded to 16 rather than 64): layer 0 starts on
 // ring slot (4 - C0M) & 3 so that its last chunk uses slot 3 and layer 1 starts on
 // slot 0 as always.
-template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1>
+template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1, int NHC = 0>
 __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, float *X0, float *Y0, int S,
                                         f32x4 *scratch, int *flags, float *lbias, int &ep, int wave, int lane,
                                         float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
@@ -1270,7 +1273,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   constexpr bool HO = TPW >= 4;
   const int t0 = wave * TPW;
   const int kb1 = HO ? t0 : 0;  // first k-chunk of every layer after the first
-  const int nh = hot.nbias / (64 * TPW);  // hidden layers; the fused head follows them
+  // hidden layers (the fused head follows them); NHC > 0: a compile-time count, the
+  // layer loop fully unrolled (a runtime loop carries the ring registers through
+  // phi copies at its head, which wait for every fragment load in flight)
+  const int nh = NHC > 0 ? NHC : hot.nbias / (64 * TPW);
   int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
 #pragma unroll
   for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
@@ -1353,6 +1359,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #endif
   float *Y = Y0;  // where the previous layer's activations go
   const float alpha = hot.hid_alpha;
+#pragma unroll(NHC > 0 ? NHC : 1)
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
     const WStream ws(w4_layer_w<TPW>(hot, l)), wn(w4_layer_w<TPW>(hot, more ? l + 1 : l));
@@ -1375,8 +1382,13 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
                                                         : nullptr;
 #endif
 #ifdef GO2PI_DIAG_WEAVE
-    // variant (diagnostics): layer l-1's epilogue of tile i+1 woven between layer l's
-    // MFMAs of chunk t0+i (measured slower: the woven VALU stretches the MFMA gaps)
+    constexpr bool WEAVE = HO;
+#else
+    constexpr bool WEAVE = false;
+#endif
+    if constexpr (WEAVE) {
+    // variant: layer l-1's epilogue of tile i+1 woven between layer l's MFMAs of
+    // chunk t0+i (register hand-off shapes only)
     act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
       float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
@@ -1398,7 +1410,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       }(std::make_integer_sequence<int, TPW>{});
     });
     publish();
-#else
+    } else {
     // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
     // publish, then layer l's MFMAs over those chunks with the B operand from registers
     // (!HO: the epilogue to LDS, then a workgroup barrier)
@@ -1420,7 +1432,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       }
     });
     if constexpr (!HO) __syncthreads();
-#endif
+    }
 #ifdef GO2PI_DIAG_CLOCK
     if (sub) sub[0] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1532,7 +1544,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 // dims = in_dim | c0 << 12 | hidden layers << 20. The LDS stride is a
 // compile-time constant; padding lanes of the observation tile read an element of
 // the same row (times a zero weight column), rows past B the last row.
-template <int TPW, int HT, int C0M, int ACTC>
+template <int TPW, int HT, int C0M, int ACTC, int NHC>
 __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *__restrict__ obs,
                                               float *__restrict__ act, const float *l0w, const float *bpack, int B,
                                               int steps, unsigned dims, unsigned *yield) {
@@ -1574,7 +1586,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
       P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    w4_step<TPW, HT, false, true, C0M, ACTC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
+    w4_step<TPW, HT, false, true, C0M, ACTC, NHC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
                                        CtlLds{}, step);
   }
 #ifdef GO2PI_DIAG_CLOCK
@@ -1939,13 +1951,13 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram 
 // The lean pipeline kernel (w4_plain_body). Argument order = preload order: the
 // first 16 dwords of the kernel arguments arrive in SGPRs (kernels_w4_t*.hip are
 // built with -amdgpu-kernarg-preload-count=16); these are 13.
-template <int TPW, int HT, int C0M, int ACTC>
+template <int TPW, int HT, int C0M, int ACTC, int NHC>
 __global__ __launch_bounds__(256) void policy_mlp_kernel(const float *__restrict__ obs, float *__restrict__ act,
                                                          const float *__restrict__ l0w,
                                                          const float *__restrict__ bpack,
                                                          const DevProgram *__restrict__ Pd, int B, int steps,
                                                          unsigned dims, unsigned *yield) {
-  w4_plain_body<TPW, HT, C0M, ACTC>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
+  w4_plain_body<TPW, HT, C0M, ACTC, NHC>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>

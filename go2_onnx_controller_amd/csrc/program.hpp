@@ -75,6 +75,7 @@ struct DevProgram {
   int w4_plain;           // pipeline, 1: no prologue / epilogue arithmetic, no recurrent cell (the lean kernel)
   int w4_c0m;             // pipeline: layer 0's k-chunks mod 4 (0 or 3; K padded to 16, not 64, when 3)
   int w4_actc;            // lean kernel: the hidden activation as a compile-time constant (1 = Elu), or -1
+  int w4_nhc;             // lean kernel: the hidden-layer count as a compile-time constant (3), or 0 (runtime)
   // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
   const float *pre_sub;
   const float *pre_div;

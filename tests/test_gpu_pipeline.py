@@ -21,15 +21,15 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 # instantiation names: policy_mlp_kernel<tiles per wave, head tiles, layer-0 chunks mod 4, hidden
-# activation (1 Elu compile-time, -1 runtime)> (the lean body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
+# activation (1 Elu compile-time, -1 runtime), hidden layers (3 compile-time, 0 runtime)> (the lean body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
 # recurrent cell (0 none / GRU, 1 LSTM)>
 # (a 33-, 40- or 48-wide observation is padded to 48 columns: 3 chunks; 70 to 128)
 SHAPES = {
-    "pipe_512_relu": "policy_mlp_kernel<8, 1, 0, -1>",
-    "pipe_256_h2": "policy_mlp_kernel<4, 2, 3, 1>",
-    "pipe_128_tanh_h2": "policy_mlp_kernel<2, 2, 3, -1>",
-    "pipe_one_hidden": "policy_mlp_kernel<4, 1, 3, 1>",
-    "go2_mlp_512": "policy_mlp_kernel<8, 1, 3, 1>",
+    "pipe_512_relu": "policy_mlp_kernel<8, 1, 0, -1, 0>",
+    "pipe_256_h2": "policy_mlp_kernel<4, 2, 3, 1, 0>",
+    "pipe_128_tanh_h2": "policy_mlp_kernel<2, 2, 3, -1, 0>",
+    "pipe_one_hidden": "policy_mlp_kernel<4, 1, 3, 1, 0>",
+    "go2_mlp_512": "policy_mlp_kernel<8, 1, 3, 1, 3>",
 }
 
 
@@ -77,7 +77,8 @@ def test_pipeline_gru_ticks(synth_path, name, kernel):
                                            ({"GO2PI_NO_PLAIN": "1"}, "policy_fused_kernel", "3"),
                                            ({"GO2PI_K0_PAD64": "1"}, "policy_mlp_kernel", "0"),
                                            ({"GO2PI_NO_PLAIN": "1", "GO2PI_K0_PAD64": "1"}, "policy_fused_kernel", "0"),
-                                           ({"GO2PI_LEAN_RT_ACT": "1"}, "policy_mlp_kernel", "3")])
+                                           ({"GO2PI_LEAN_RT_ACT": "1"}, "policy_mlp_kernel", "3"),
+                                           ({"GO2PI_LEAN_RT_NH": "1"}, "policy_mlp_kernel", "3")])
 @pytest.mark.parametrize("name", ["go2_mlp_512", "pipe_128_tanh_h2", "pipe_256_h2"])
 def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, kname, c0m):
     """The lean body (no prologue / epilogue) and the general one, each with layer 0
@@ -93,9 +94,12 @@ def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, k
     x = np.random.default_rng(11).standard_normal((4096, g.inputs[0][1][1])).astype(np.float32)
     with Engine(p, max_batch=4096, small_batch=-1) as e:
         k = e.batched_kernel
-        args = k[k.index("<") + 1:-1].split(", ")  # mlp: <tpw, ht, c0m, act>; fused: <waves, tpw, ht, c0m, rnn>
+        args = k[k.index("<") + 1:-1].split(", ")  # mlp: <tpw, ht, c0m, act, nh>; fused: <waves, tpw, ht, c0m, rnn>
         assert k.startswith(kname) and args[2 if kname == "policy_mlp_kernel" else 3] == c0m, k
         if "GO2PI_LEAN_RT_ACT" in env:
             assert args[3] == "-1", k
+        if kname == "policy_mlp_kernel":  # the compile-time layer count only with Elu, 3 hidden layers
+            nhc = "3" if name == "go2_mlp_512" and not {"GO2PI_LEAN_RT_ACT", "GO2PI_LEAN_RT_NH"} & set(env) else "0"
+            assert args[4] == nhc, k
         for B in (5, 16, 4096):
             assert abs_err(e.run(x[:B]), onnx_ref.act(g, x[:B])) <= TOL, (B, env)
