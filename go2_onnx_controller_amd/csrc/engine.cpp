@@ -780,7 +780,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
                  std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) && p.clip_hi > 0 &&
                  p.scale == 1.f && p.lds_stride == 64 * p.w4_tpw + 4 && !std::getenv("GO2PI_NO_PLAIN");
     // the lean kernel's compile-time activation: Elu (the exported rsl_rl / Isaac policies'), else runtime
-    p.w4_actc = (p.hid_act == 1 && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B diagnostics only
+    // (1 = Elu with alpha 1, the ONNX default; any other alpha takes the runtime form)
+    p.w4_actc = (p.hid_act == 1 && p.hid_alpha == 1.f && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B only
     // ... and its hidden-layer count (3: the usual policy depth): the layer loop fully
     // unrolled, so no ring-register copies (and no vmcnt(0)) at the layer boundaries
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only

@@ -828,6 +828,33 @@ __device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const fl
   return v;
 }
 
+// The lean kernel's Elu epilogue (ACTC == 1: Elu with alpha = 1, the exported
+// policies'): the bias is already in the accumulator (BIN: the first MFMA of each
+// tile took it as its C operand), and the x * log2(e) and e - 1 steps run as
+// packed pairs. Per element the same operations as act_t<1> with alpha = 1
+// (x > 0 ? x : exp2(x * log2 e) - 1), so the same bits for the same x.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool BIN>
+__device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv) {
+  f32x2 x01 = {acc[0], acc[1]}, x23 = {acc[2], acc[3]};
+  if constexpr (!BIN) {
+    x01 += f32x2{bv.x, bv.y};
+    x23 += f32x2{bv.z, bv.w};
+  }
+  const f32x2 L = {1.4426950408889634f, 1.4426950408889634f};
+  const f32x2 t01 = x01 * L, t23 = x23 * L;
+  f32x2 e01 = {__builtin_amdgcn_exp2f(t01.x), __builtin_amdgcn_exp2f(t01.y)};
+  f32x2 e23 = {__builtin_amdgcn_exp2f(t23.x), __builtin_amdgcn_exp2f(t23.y)};
+  e01 -= 1.f;
+  e23 -= 1.f;
+  float4 v;
+  v.x = x01.x > 0.f ? x01.x : e01.x;
+  v.y = x01.y > 0.f ? x01.y : e01.y;
+  v.z = x23.x > 0.f ? x23.x : e23.x;
+  v.w = x23.y > 0.f ? x23.y : e23.y;
+  return v;
+}
+
 // One own-phase chunk: the MFMAs of chunk I (B operand b = the epilogue value of
 // the previous layer's tile t0 + I, from registers) with the epilogue of tile
 // I + 1 (accumulator pa, bias pb) woven between them when NEXT. The epilogue is
@@ -1271,6 +1298,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   // short to cover the other waves' epilogues, and an epilogue + barrier + natural
   // chunk order measured faster (9.9 vs 11.0 us per 4096-robot step)
   constexpr bool HO = TPW >= 4;
+  // the lean Elu kernel: each hidden layer's bias enters as the C operand of the
+  // tile's first MFMA (the fp32 chain starts at b instead of adding it after the
+  // sum), and the epilogue is w4_epi_elu1
+  constexpr bool BIN = PL && ACTC == 1;
   const int t0 = wave * TPW;
   const int kb1 = HO ? t0 : 0;  // first k-chunk of every layer after the first
   // hidden layers (the fused head follows them); NHC > 0: a compile-time count, the
@@ -1335,12 +1366,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   if (nh == 1) load_head();
   // layer 0: the observation tile, natural chunk order; the tail fetches layer 1's own chunks
   f32x4 acc[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float *brow = lbias + t0 * 16 + ((lane >> 4) << 2);  // this lane's bias float4 of tile t0, layer 0
   float4 bv[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) bv[i] = *reinterpret_cast<const float4 *>(brow + i * 16);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = BIN ? f32x4{bv[i].x, bv[i].y, bv[i].z, bv[i].w} : f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const WStream ws(hot.l0w);
     if (nh > 1) {
@@ -1363,12 +1394,13 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
     const WStream ws(w4_layer_w<TPW>(hot, l)), wn(w4_layer_w<TPW>(hot, more ? l + 1 : l));
-    f32x4 accn[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) accn[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 bvn[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) bvn[i] = *reinterpret_cast<const float4 *>(brow + l * CH * 16 + i * 16);
+    f32x4 accn[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+      accn[i] = BIN ? f32x4{bvn[i].x, bvn[i].y, bvn[i].z, bvn[i].w} : f32x4{0.f, 0.f, 0.f, 0.f};
     float *yrow = Y + (lane & 15) * S + t0 * 16 + ((lane >> 4) << 2);
     // publish this wave's layer l-1 tiles (after its own LDS stores) for the other waves
     auto publish = [&] {
@@ -1382,7 +1414,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
                                                         : nullptr;
 #endif
 #ifdef GO2PI_DIAG_WEAVE
-    constexpr bool WEAVE = HO;
+    constexpr bool WEAVE = HO && !BIN;
 #else
     constexpr bool WEAVE = false;
 #endif
@@ -1418,7 +1450,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       constexpr int ACT = decltype(act_k)::value;
       float4 v[TPW];
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
+      for (int i = 0; i < TPW; ++i) {
+        if constexpr (ACTC == 1 && PL) v[i] = w4_epi_elu1<BIN>(acc[i], bv[i]);
+        else v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
+      }
 #pragma unroll
       for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
 #ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
@@ -1484,7 +1519,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       constexpr int ACT = decltype(act_k)::value;
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
-        const float4 v = w4_epi<ACT>(alpha, acc[i], bv[i]);
+        float4 v;
+        if constexpr (ACTC == 1 && PL) v = w4_epi_elu1<BIN>(acc[i], bv[i]);
+        else v = w4_epi<ACT>(alpha, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
 #pragma unroll
