@@ -841,6 +841,10 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
     x01 += f32x2{bv.x, bv.y};
     x23 += f32x2{bv.z, bv.w};
   }
+  // one copy out of the accumulator registers per element (the scheduler otherwise
+  // re-reads an AGPR for the select; VALU here is not hidden behind the MFMAs:
+  // tools/mfma_valu.hip, every instruction counts)
+  asm volatile("" : "+v"(x01), "+v"(x23));
   const f32x2 L = {1.4426950408889634f, 1.4426950408889634f};
   const f32x2 t01 = x01 * L, t23 = x23 * L;
   f32x2 e01 = {__builtin_amdgcn_exp2f(t01.x), __builtin_amdgcn_exp2f(t01.y)};
