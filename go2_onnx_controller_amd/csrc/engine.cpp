@@ -783,8 +783,12 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     // (1 = Elu with alpha 1, the ONNX default; any other alpha takes the runtime form)
     p.w4_actc = (p.hid_act == 1 && p.hid_alpha == 1.f && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B only
     // ... and its hidden-layer count (3: the usual policy depth): the layer loop fully
-    // unrolled, so no ring-register copies (and no vmcnt(0)) at the layer boundaries
+    // unrolled, so no ring-register copies (and no vmcnt(0)) at the layer boundaries.
+    // The general body (GRU policies) takes both only together; LSTM policies neither.
+    const bool lstm = p.has_gru && p.gru.cell == 1;
+    if (lstm) p.w4_actc = -1;
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
+    if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
   }
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
@@ -1285,8 +1289,9 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
                                 // act, hidden layers>
       std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
     else
-      std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d>", e->waves, t, h, c0m,
-                    (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0);
+      std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d, %d, %d>", e->waves, t, h, c0m,
+                    (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0, t ? e->prog.w4_actc : -1,
+                    t ? e->prog.w4_nhc : 0);
     return GO2PI_OK;
   });
 }

@@ -1302,10 +1302,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   // short to cover the other waves' epilogues, and an epilogue + barrier + natural
   // chunk order measured faster (9.9 vs 11.0 us per 4096-robot step)
   constexpr bool HO = TPW >= 4;
-  // the lean Elu kernel: each hidden layer's bias enters as the C operand of the
-  // tile's first MFMA (the fp32 chain starts at b instead of adding it after the
-  // sum), and the epilogue is w4_epi_elu1
-  constexpr bool BIN = PL && ACTC == 1;
+  // compile-time Elu (alpha 1): each hidden layer's bias enters as the C operand of
+  // the tile's first MFMA (the fp32 chain starts at b instead of adding it after
+  // the sum), and the epilogue is w4_epi_elu1
+  constexpr bool BIN = ACTC == 1;
   const int t0 = wave * TPW;
   const int kb1 = HO ? t0 : 0;  // first k-chunk of every layer after the first
   // hidden layers (the fused head follows them); NHC > 0: a compile-time count, the
@@ -1455,7 +1455,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       float4 v[TPW];
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
-        if constexpr (ACTC == 1 && PL) v[i] = w4_epi_elu1<BIN>(acc[i], bv[i]);
+        if constexpr (ACTC == 1) v[i] = w4_epi_elu1<BIN>(acc[i], bv[i]);
         else v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
       }
 #pragma unroll
@@ -1524,7 +1524,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         float4 v;
-        if constexpr (ACTC == 1 && PL) v = w4_epi_elu1<BIN>(acc[i], bv[i]);
+        if constexpr (ACTC == 1) v = w4_epi_elu1<BIN>(acc[i], bv[i]);
         else v = w4_epi<ACT>(alpha, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
@@ -1640,7 +1640,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
 
 // RNN: the recurrent cell this instantiation runs when the program has one (0 GRU,
 // 1 LSTM; one kernel per cell keeps the other cell's registers out of it).
-template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
+template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0, int ACTC = -1, int NHC = 0>
 __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
                                            float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
                                            const DevCtl ctl) {
@@ -1865,7 +1865,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
                  bufB[tid * S + 1], bufB[tid * S + 255], S, H, P.in_pad, P.has_gru);
 #endif
       }
-      w4_step<W4T, W4H, CTL, false, C0M>(P, w4_hot(P), X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv,
+      w4_step<W4T, W4H, CTL, false, C0M, ACTC, NHC>(P, w4_hot(P), X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv,
                                          row0, B, ctl, CL,
                              step);
       continue;
@@ -1981,12 +1981,12 @@ template <int TPW>
 int w4_launch_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, float *hidden, int batch,
                   void *stream);
 
-template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
+template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0, int ACTC = -1, int NHC = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram *__restrict__ Pd,
                                                                const float *__restrict__ obs,
                                                                float *__restrict__ act, float *__restrict__ hidden,
                                                                int B, int steps) {
-  fused_body<NW, false, W4T, W4H, C0M, RNN>(*Pd, obs, act, hidden, B, steps, DevCtl{});
+  fused_body<NW, false, W4T, W4H, C0M, RNN, ACTC, NHC>(*Pd, obs, act, hidden, B, steps, DevCtl{});
 }
 
 // The lean pipeline kernel (w4_plain_body). Argument order = preload order: the

@@ -35,10 +35,10 @@ def _rollout(path, xs, h0=None, c0=None):
     return np.stack(ys), h[0], c[0]
 
 
-@pytest.mark.parametrize("name,waves,kernel", [("lstm_small", 0, "policy_fused_kernel<8, 0, 0, 0, 1>"),
-                                               ("lstm_128", 0, "policy_fused_kernel<4, 4, 1, 0, 1>"),
-                                               ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1>"),
-                                               ("go2_lstm_256", 8, "policy_fused_kernel<8, 0, 0, 0, 1>")])
+@pytest.mark.parametrize("name,waves,kernel", [("lstm_small", 0, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>"),
+                                               ("lstm_128", 0, "policy_fused_kernel<4, 4, 1, 0, 1, -1, 0>"),
+                                               ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1, -1, 0>"),
+                                               ("go2_lstm_256", 8, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>")])
 @pytest.mark.parametrize("B", [1, 37, 4096])
 def test_lstm_ticks(synth_path, name, waves, kernel, B):
     from go2_onnx_controller_amd import Engine

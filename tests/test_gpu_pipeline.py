@@ -22,7 +22,7 @@ TOL = 1e-5
 
 # instantiation names: policy_mlp_kernel<tiles per wave, head tiles, layer-0 chunks mod 4, hidden
 # activation (1 Elu compile-time, -1 runtime), hidden layers (3 compile-time, 0 runtime)> (the lean body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
-# recurrent cell (0 none / GRU, 1 LSTM)>
+# recurrent cell (0 none / GRU, 1 LSTM), act, hidden layers>
 # (a 33-, 40- or 48-wide observation is padded to 48 columns: 3 chunks; 70 to 128)
 SHAPES = {
     "pipe_512_relu": "policy_mlp_kernel<8, 1, 0, -1, 0>",
@@ -43,20 +43,25 @@ def test_pipeline_shapes(synth_path, name):
     x = np.random.default_rng(7).standard_normal((300, in_dim)).astype(np.float32)
     with Engine(p, max_batch=512, small_batch=-1) as e, Engine(p, max_batch=512, waves=8, small_batch=-1) as gen:
         assert e.batched_kernel == SHAPES[name]
-        assert gen.batched_kernel == "policy_fused_kernel<8, 0, 0, 0, 0>"
+        assert gen.batched_kernel == "policy_fused_kernel<8, 0, 0, 0, 0, -1, 0>"
         for B in (1, 16, 17, 300):
             want = onnx_ref.act(g, x[:B])
             assert abs_err(e.run(x[:B]), want) <= TOL, (name, B)
             assert abs_err(gen.run(x[:B]), want) <= TOL, (name, B)
 
 
-@pytest.mark.parametrize("name,kernel", [("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0>"),
-                                         ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0>")])
-def test_pipeline_gru_ticks(synth_path, name, kernel):
+@pytest.mark.parametrize("name,kernel,env", [("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, 1, 3>", {}),
+                                             ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, -1, 0>",
+                                              {"GO2PI_LEAN_RT_NH": "1"}),
+                                             ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0, -1, 0>", {})])
+def test_pipeline_gru_ticks(synth_path, monkeypatch, name, kernel, env):
     """GRU front stage + MLP pipeline over several ticks (hidden state carried by
-    the engine), against the fp64 ONNX GRU oracle, actions and hidden state."""
+    the engine), against the fp64 ONNX GRU oracle, actions and hidden state; the
+    dense layers with the compile-time Elu and layer count, and the runtime forms."""
     from go2_onnx_controller_amd import Engine
     from oracle import onnx_ref
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     p = synth_path(name)
     g = onnx_ref.load(p)
     I, H = g.inputs[0][1][1], g.inputs[1][1][2]
