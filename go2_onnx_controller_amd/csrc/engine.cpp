@@ -773,6 +773,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.hid_alpha = p.L[0].alpha;
     p.head_act = H.act;
     p.head_alpha = H.alpha;
+    p.post_plain = (!p.post_tanh && std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) &&
+                    p.clip_hi > 0 && p.scale == 1.f) ? 1 : 0;
     p.w4_c0m = p.c0 % 4;
     // the lean kernel: no prologue / epilogue arithmetic, no recurrent cell, and an
     // LDS row no wider than the hidden layers
@@ -784,9 +786,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.w4_actc = (p.hid_act == 1 && p.hid_alpha == 1.f && !std::getenv("GO2PI_LEAN_RT_ACT")) ? 1 : -1;  // env: A/B only
     // ... and its hidden-layer count (3: the usual policy depth): the layer loop fully
     // unrolled, so no ring-register copies (and no vmcnt(0)) at the layer boundaries.
-    // The general body (GRU policies) takes both only together; LSTM policies neither.
-    const bool lstm = p.has_gru && p.gru.cell == 1;
-    if (lstm) p.w4_actc = -1;
+    // The general body (recurrent policies) takes both only together.
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
     if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
   }

@@ -1252,11 +1252,12 @@ struct W4Hot {
   unsigned *err;
   int nbias, head_n, c0, hid_act, head_act;
   float hid_alpha, head_alpha;
+  int post_plain;
 };
 
 __device__ __forceinline__ W4Hot w4_hot(const DevProgram &P) {
   return W4Hot{P.l0_w,     P.head_w,  P.head_bias, P.bpack,    P.err_hot,   P.nbias,
-               P.head_n,   P.c0,      P.hid_act,   P.head_act, P.hid_alpha, P.head_alpha};
+               P.head_n,   P.c0,      P.hid_act,   P.head_act, P.hid_alpha, P.head_alpha, P.post_plain};
 }
 
 // f(integral_constant<activation>): A >= 0 a compile-time activation (the lean
@@ -1551,14 +1552,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) hs[0] += scratch[(wave * 4 + w) * 64 + lane];
-    if constexpr (PL) {
-      // no epilogue: activation (usually none) and the plain store of the valid rows / columns
+    // no action post-processing (the lean kernel; a general-body program without
+    // tanh / clip / scale, e.g. a GRU policy): the head's activation (usually none)
+    // and the plain store of the valid rows / columns, from the hot fields
+    if (PL || (!CTL && hot.post_plain)) {
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
       with_act(hot.head_act, [&](auto act_k) {
         constexpr int ACT = decltype(act_k)::value;
         const float4 v = w4_epi<ACT>(hot.head_alpha, hs[0], hbv[0]);
-        if (row < B) {  // (ac: the action rows of all steps; this step's start at step * B rows)
-          float *o = ac + ((size_t)step * B + row) * hot.head_n;
+        if (row < B) {  // (lean kernel: ac = the action rows of all steps, this step's at step * B
+                        // rows; general body: ac = this step's rows already)
+          float *o = ac + ((PL ? (size_t)step * B : (size_t)0) + row) * hot.head_n;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (n0 + r < hot.head_n) o[n0 + r] = f4c(v, r);
@@ -1595,7 +1599,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)(dims >> 20);
   // (the program's fields are read inside w4_step once the first loads are out)
-  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f};
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f, 1};
   constexpr int S = 64 * TPW + 4;  // = P.lds_stride (the engine selects this kernel only then)
   float *bufA = lds, *bufB = lds + GO2PI_TILE_ROWS * S;
   f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + 2 * GO2PI_TILE_ROWS * S);

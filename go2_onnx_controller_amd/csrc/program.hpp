@@ -62,6 +62,7 @@ struct DevProgram {
   int in_dim_hot;          // = in_dim
   int hid_act, head_act;   // activation of every hidden layer (uniform), of the head
   float hid_alpha, head_alpha;
+  int post_plain;          // 1: no action post-processing (tanh / clip / scale): the head's plain store
   // ---- the rest
   int nl;
   int in_dim, in_pad, out_dim;

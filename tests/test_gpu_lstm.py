@@ -37,7 +37,7 @@ def _rollout(path, xs, h0=None, c0=None):
 
 @pytest.mark.parametrize("name,waves,kernel", [("lstm_small", 0, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>"),
                                                ("lstm_128", 0, "policy_fused_kernel<4, 4, 1, 0, 1, -1, 0>"),
-                                               ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1, -1, 0>"),
+                                               ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1, 1, 3>"),
                                                ("go2_lstm_256", 8, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>")])
 @pytest.mark.parametrize("B", [1, 37, 4096])
 def test_lstm_ticks(synth_path, name, waves, kernel, B):
