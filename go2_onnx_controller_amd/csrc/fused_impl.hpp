@@ -1035,81 +1035,106 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
   int vo[GT];                     // per-lane byte offset of tile t0 + i's z fragment in chunk 0 (r +1 KiB, n +2 KiB)
 #pragma unroll
   for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 3 * 64 + lane) * 16;
-  float4 f[4][NF];
-  asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
-#pragma unroll
-  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
-  wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
+  // x chunks that hold data: Cxe = ceil(I / 16) (the packing pads x to whole 4-chunk
+  // groups; a 48-wide observation leaves chunk 3 all zeros, skipped here: its 4 * NF
+  // MFMAs are 1/20 of GRU-256's stage). With Cxe = 3 mod 4 the ring starts on slot 1
+  // so that the h chunks start on slot 0 and keep their 4-chunk groups.
+  const int Cxe = (G.I + 15) >> 4;
   f32x4 z[GT], r[GT], nx[GT], nh[GT];
   float4 bz[GT], br[GT], bx[GT], bh[GT];
-#pragma unroll
-  for (int i = 0; i < GT; ++i) {
-    const int j = (t0 + i) * 16 + u0;
-    bz[i] = *reinterpret_cast<const float4 *>(G.bzr + j);
-    br[i] = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
-    bx[i] = *reinterpret_cast<const float4 *>(G.bh + j);
-    bh[i] = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
-    z[i] = r[i] = nx[i] = nh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   const float *xrow = X + (lane & 15) * xs + u0;
   const float *hrow = Hs + (lane & 15) * xs + u0;
-  float4 a[2];
-  a[0] = *reinterpret_cast<const float4 *>(xrow);
-  // chunk c (slot S = c & 3); XPH: an x chunk (the third gate accumulates n_x, else
-  // n_h); NEXT: chunk c + 1 exists (its B operand and fragments are fetched here);
-  // NX: chunk c + 1 is an x chunk (else an h chunk). One fixed source row per
-  // instantiation keeps the B-operand read a single ds_read_b128.
-  auto chunk = [&](auto s_k, auto xph_k, auto next_k, auto nx_k, int c) {
-    constexpr int S = decltype(s_k)::value;
-    constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
-    if constexpr (NEXT) {
-      if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (c + 1) * 16);
-      else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (c + 1 - Cx) * 16);
-    }
-    const float4 b = a[S & 1];
+  auto run = [&](auto k0_k) {
+    constexpr int K0S = decltype(k0_k)::value;  // ring slot of chunk 0
+    float4 f[4][NF];
+    asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      const int jk = m / NF, i = (m % NF) / 3, g = m % 3;
-      const float wv = f4c(f[S][i * 3 + g], jk), bk = f4c(b, jk);
-      if (g == 0) z[i] = mfma4(wv, bk, z[i]);
-      else if (g == 1) r[i] = mfma4(wv, bk, r[i]);
-      else if (XPH) nx[i] = mfma4(wv, bk, nx[i]);
-      else nh[i] = mfma4(wv, bk, nh[i]);
-      if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
-        const int q = m >> 1;
-        __builtin_amdgcn_sched_barrier(0);
-        f[(S + 1) & 3][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, (c + 1) * csb);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < NF; ++q) f[K0S][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, 0);
+    wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      const int j = (t0 + i) * 16 + u0;
+      bz[i] = *reinterpret_cast<const float4 *>(G.bzr + j);
+      br[i] = *reinterpret_cast<const float4 *>(G.bzr + G.H + j);
+      bx[i] = *reinterpret_cast<const float4 *>(G.bh + j);
+      bh[i] = *reinterpret_cast<const float4 *>(G.bh + G.H + j);
+      z[i] = r[i] = nx[i] = nh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float4 a[2];
+    a[K0S & 1] = *reinterpret_cast<const float4 *>(xrow);
+    // chunk c (slot S); XPH: an x chunk (the third gate accumulates n_x, else n_h);
+    // NEXT: a chunk follows, cn (its B operand and fragments are fetched here); NX:
+    // that chunk is an x chunk (else an h chunk). One fixed source row per
+    // instantiation keeps the B-operand read a single ds_read_b128.
+    auto chunk = [&](auto s_k, auto xph_k, auto next_k, auto nx_k, int c, int cn) {
+      constexpr int S = decltype(s_k)::value;
+      constexpr bool XPH = decltype(xph_k)::value, NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
+      if constexpr (NEXT) {
+        if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + cn * 16);
+        else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (cn - Cx) * 16);
+      }
+      const float4 b = a[S & 1];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int jk = m / NF, i = (m % NF) / 3, g = m % 3;
+        const float wv = f4c(f[S][i * 3 + g], jk), bk = f4c(b, jk);
+        if (g == 0) z[i] = mfma4(wv, bk, z[i]);
+        else if (g == 1) r[i] = mfma4(wv, bk, r[i]);
+        else if (XPH) nx[i] = mfma4(wv, bk, nx[i]);
+        else nh[i] = mfma4(wv, bk, nh[i]);
+        if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
+          const int q = m >> 1;
+          __builtin_amdgcn_sched_barrier(0);
+          f[(S + 1) & 3][q] = ws.ld(vo[q / 3] + (q % 3) * 1024, cn * csb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    int c = 0;
+    if constexpr (K0S == 1) {  // a leading group of 3 x chunks (slots 1-3)
+      if (Cxe > 3) {
+        chunk(I1{}, T_{}, T_{}, T_{}, 0, 1);
+        chunk(I2{}, T_{}, T_{}, T_{}, 1, 2);
+        chunk(I3{}, T_{}, T_{}, T_{}, 2, 3);
+        c = 3;
+      } else {
+        chunk(I1{}, T_{}, T_{}, T_{}, 0, 1);
+        chunk(I2{}, T_{}, T_{}, T_{}, 1, 2);
+        chunk(I3{}, T_{}, T_{}, F_{}, 2, Cx);  // the next chunk is the first h chunk
+        c = Cxe;
       }
     }
+    if (c < Cxe) {
+      for (; c + 4 < Cxe; c += 4) {
+        chunk(I0{}, T_{}, T_{}, T_{}, c, c + 1);
+        chunk(I1{}, T_{}, T_{}, T_{}, c + 1, c + 2);
+        chunk(I2{}, T_{}, T_{}, T_{}, c + 2, c + 3);
+        chunk(I3{}, T_{}, T_{}, T_{}, c + 3, c + 4);
+      }
+      chunk(I0{}, T_{}, T_{}, T_{}, c, c + 1);
+      chunk(I1{}, T_{}, T_{}, T_{}, c + 1, c + 2);
+      chunk(I2{}, T_{}, T_{}, T_{}, c + 2, c + 3);
+      chunk(I3{}, T_{}, T_{}, F_{}, c + 3, Cx);  // the next chunk is the first h chunk
+    }
+    for (c = Cx; c + 4 < Cx + Ch; c += 4) {
+      chunk(I0{}, F_{}, T_{}, F_{}, c, c + 1);
+      chunk(I1{}, F_{}, T_{}, F_{}, c + 1, c + 2);
+      chunk(I2{}, F_{}, T_{}, F_{}, c + 2, c + 3);
+      chunk(I3{}, F_{}, T_{}, F_{}, c + 3, c + 4);
+    }
+    chunk(I0{}, F_{}, T_{}, F_{}, c, c + 1);
+    chunk(I1{}, F_{}, T_{}, F_{}, c + 1, c + 2);
+    chunk(I2{}, F_{}, T_{}, F_{}, c + 2, c + 3);
+    chunk(I3{}, F_{}, F_{}, F_{}, c + 3, c + 3);
   };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  int c = 0;
-  for (; c + 4 < Cx; c += 4) {
-    chunk(I0{}, T_{}, T_{}, T_{}, c);
-    chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
-    chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
-    chunk(I3{}, T_{}, T_{}, T_{}, c + 3);
-  }
-  chunk(I0{}, T_{}, T_{}, T_{}, c);
-  chunk(I1{}, T_{}, T_{}, T_{}, c + 1);
-  chunk(I2{}, T_{}, T_{}, T_{}, c + 2);
-  chunk(I3{}, T_{}, T_{}, F_{}, c + 3);  // the next chunk is the first h chunk
-  for (c = Cx; c + 4 < Cx + Ch; c += 4) {
-    chunk(I0{}, F_{}, T_{}, F_{}, c);
-    chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
-    chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
-    chunk(I3{}, F_{}, T_{}, F_{}, c + 3);
-  }
-  chunk(I0{}, F_{}, T_{}, F_{}, c);
-  chunk(I1{}, F_{}, T_{}, F_{}, c + 1);
-  chunk(I2{}, F_{}, T_{}, F_{}, c + 2);
-  chunk(I3{}, F_{}, F_{}, F_{}, c + 3);
+  if ((Cxe & 3) == 3) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 0>{});
 #ifdef GO2PI_DIAG_CLOCK
   if (st && wave == 0 && lane == 0) st[44] = __builtin_amdgcn_s_memtime();
 #endif
