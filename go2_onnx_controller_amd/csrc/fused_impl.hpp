@@ -1179,68 +1179,91 @@ __device__ __forceinline__ void w4_lstm(const DevGru &G, const float *X, const f
   int vo[GT];
 #pragma unroll
   for (int i = 0; i < GT; ++i) vo[i] = ((t0 + i) * 4 * 64 + lane) * 16;
-  float4 f[4][NF];
-  asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
-#pragma unroll
-  for (int q = 0; q < NF; ++q) f[0][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, 0);
-  wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
+  // x chunks that hold data (as w4_gru: the all-zero padding chunk is skipped)
+  const int Cxe = (G.I + 15) >> 4;
   f32x4 acc[4][GT];
-#pragma unroll
-  for (int i = 0; i < GT; ++i)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float *xrow = X + (lane & 15) * xs + u0;
   const float *hrow = Hs + (lane & 15) * xs + u0;
-  float4 a[2];
-  a[0] = *reinterpret_cast<const float4 *>(xrow);
-  // chunk c (slot S = c & 3); NEXT: chunk c + 1 exists; NX: chunk c + 1 is an x chunk
-  auto chunk = [&](auto s_k, auto next_k, auto nx_k, int cc) {
-    constexpr int S = decltype(s_k)::value;
-    constexpr bool NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
-    if constexpr (NEXT) {
-      if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + (cc + 1) * 16);
-      else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (cc + 1 - Cx) * 16);
-    }
-    const float4 b = a[S & 1];
+  auto run = [&](auto k0_k) {
+    constexpr int K0S = decltype(k0_k)::value;  // ring slot of chunk 0
+    float4 f[4][NF];
+    asm volatile("" ::: "memory");  // the caller's LDS-DMA stays ahead of the NF loads
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      const int jk = m / NF, i = (m % NF) / 4, g = m % 4;
-      acc[g][i] = mfma4(f4c(f[S][i * 4 + g], jk), f4c(b, jk), acc[g][i]);
-      if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
-        const int q = m >> 1;
-        __builtin_amdgcn_sched_barrier(0);
-        f[(S + 1) & 3][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, (cc + 1) * csb);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < NF; ++q) f[K0S][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, 0);
+    wg_barrier_vm<NF>();  // the x / h rows (LDS-DMA) have landed; chunk 0's fragments stay in flight
+#pragma unroll
+    for (int i = 0; i < GT; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 a[2];
+    a[K0S & 1] = *reinterpret_cast<const float4 *>(xrow);
+    // chunk cc (slot S); NEXT: a chunk follows, cn; NX: cn is an x chunk
+    auto chunk = [&](auto s_k, auto next_k, auto nx_k, int cc, int cn) {
+      constexpr int S = decltype(s_k)::value;
+      constexpr bool NEXT = decltype(next_k)::value, NX = decltype(nx_k)::value;
+      if constexpr (NEXT) {
+        if constexpr (NX) a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(xrow + cn * 16);
+        else a[(S + 1) & 1] = *reinterpret_cast<const float4 *>(hrow + (cn - Cx) * 16);
+      }
+      const float4 b = a[S & 1];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int jk = m / NF, i = (m % NF) / 4, g = m % 4;
+        acc[g][i] = mfma4(f4c(f[S][i * 4 + g], jk), f4c(b, jk), acc[g][i]);
+        if (NEXT && (m & 1) == 1 && (m >> 1) < NF) {
+          const int q = m >> 1;
+          __builtin_amdgcn_sched_barrier(0);
+          f[(S + 1) & 3][q] = ws.ld(vo[q / 4] + (q % 4) * 1024, cn * csb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      (void)cc;
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    int cc = 0;
+    if constexpr (K0S == 1) {  // a leading group of 3 x chunks (slots 1-3)
+      if (Cxe > 3) {
+        chunk(I1{}, T_{}, T_{}, 0, 1);
+        chunk(I2{}, T_{}, T_{}, 1, 2);
+        chunk(I3{}, T_{}, T_{}, 2, 3);
+        cc = 3;
+      } else {
+        chunk(I1{}, T_{}, T_{}, 0, 1);
+        chunk(I2{}, T_{}, T_{}, 1, 2);
+        chunk(I3{}, T_{}, F_{}, 2, Cx);  // the next chunk is the first h chunk
+        cc = Cxe;
       }
     }
+    if (cc < Cxe) {
+      for (; cc + 4 < Cxe; cc += 4) {
+        chunk(I0{}, T_{}, T_{}, cc, cc + 1);
+        chunk(I1{}, T_{}, T_{}, cc + 1, cc + 2);
+        chunk(I2{}, T_{}, T_{}, cc + 2, cc + 3);
+        chunk(I3{}, T_{}, T_{}, cc + 3, cc + 4);
+      }
+      chunk(I0{}, T_{}, T_{}, cc, cc + 1);
+      chunk(I1{}, T_{}, T_{}, cc + 1, cc + 2);
+      chunk(I2{}, T_{}, T_{}, cc + 2, cc + 3);
+      chunk(I3{}, T_{}, F_{}, cc + 3, Cx);  // the next chunk is the first h chunk
+    }
+    for (cc = Cx; cc + 4 < Cx + Ch; cc += 4) {
+      chunk(I0{}, T_{}, F_{}, cc, cc + 1);
+      chunk(I1{}, T_{}, F_{}, cc + 1, cc + 2);
+      chunk(I2{}, T_{}, F_{}, cc + 2, cc + 3);
+      chunk(I3{}, T_{}, F_{}, cc + 3, cc + 4);
+    }
+    chunk(I0{}, T_{}, F_{}, cc, cc + 1);
+    chunk(I1{}, T_{}, F_{}, cc + 1, cc + 2);
+    chunk(I2{}, T_{}, F_{}, cc + 2, cc + 3);
+    chunk(I3{}, F_{}, F_{}, cc + 3, cc + 3);
   };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  int cc = 0;
-  for (; cc + 4 < Cx; cc += 4) {
-    chunk(I0{}, T_{}, T_{}, cc);
-    chunk(I1{}, T_{}, T_{}, cc + 1);
-    chunk(I2{}, T_{}, T_{}, cc + 2);
-    chunk(I3{}, T_{}, T_{}, cc + 3);
-  }
-  chunk(I0{}, T_{}, T_{}, cc);
-  chunk(I1{}, T_{}, T_{}, cc + 1);
-  chunk(I2{}, T_{}, T_{}, cc + 2);
-  chunk(I3{}, T_{}, F_{}, cc + 3);  // the next chunk is the first h chunk
-  for (cc = Cx; cc + 4 < Cx + Ch; cc += 4) {
-    chunk(I0{}, T_{}, F_{}, cc);
-    chunk(I1{}, T_{}, F_{}, cc + 1);
-    chunk(I2{}, T_{}, F_{}, cc + 2);
-    chunk(I3{}, T_{}, F_{}, cc + 3);
-  }
-  chunk(I0{}, T_{}, F_{}, cc);
-  chunk(I1{}, T_{}, F_{}, cc + 1);
-  chunk(I2{}, T_{}, F_{}, cc + 2);
-  chunk(I3{}, F_{}, F_{}, cc + 3);
+  if ((Cxe & 3) == 3) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 0>{});
   float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
