@@ -833,6 +833,13 @@ __device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const fl
 // tile took it as its C operand), and the x * log2(e) and e - 1 steps run as
 // packed pairs. Per element the same operations as act_t<1> with alpha = 1
 // (x > 0 ? x : exp2(x * log2 e) - 1), so the same bits for the same x.
+//
+// GO2PI_DIAG_ELUMAX (diagnostics, not shipped): the select folded away — e =
+// exp2(x * log2 e) clamped to [0, 1] (the v_exp_f32 clamp bit) is exp(min(x, 0)),
+// and Elu(x) = max(x, e - 1). 35.51 -> 35.37 us at mlp512 (profiles/
+// r03_ab_elumax.json), but the clamp maps a NaN to 0 (DX10 clamp mode), so
+// Elu(NaN) becomes -1 where ONNX Elu propagates the NaN; and in IEEE mode each
+// fmaxf also quiets its register operand (a second v_max per element).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool BIN>
 __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv) {
@@ -847,6 +854,16 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
   asm volatile("" : "+v"(x01), "+v"(x23));
   const f32x2 L = {1.4426950408889634f, 1.4426950408889634f};
   const f32x2 t01 = x01 * L, t23 = x23 * L;
+#ifdef GO2PI_DIAG_ELUMAX
+  // (fmed3(v, 0, 1) folds into the exp's clamp bit)
+  f32x2 e01 = {__builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t01.x), 0.f, 1.f),
+               __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t01.y), 0.f, 1.f)};
+  f32x2 e23 = {__builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t23.x), 0.f, 1.f),
+               __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t23.y), 0.f, 1.f)};
+  e01 -= 1.f;
+  e23 -= 1.f;
+  return make_float4(fmaxf(x01.x, e01.x), fmaxf(x01.y, e01.y), fmaxf(x23.x, e23.x), fmaxf(x23.y, e23.y));
+#else
   f32x2 e01 = {__builtin_amdgcn_exp2f(t01.x), __builtin_amdgcn_exp2f(t01.y)};
   f32x2 e23 = {__builtin_amdgcn_exp2f(t23.x), __builtin_amdgcn_exp2f(t23.y)};
   e01 -= 1.f;
@@ -857,6 +874,7 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
   v.z = x23.x > 0.f ? x23.x : e23.x;
   v.w = x23.y > 0.f ? x23.y : e23.y;
   return v;
+#endif
 }
 
 // One own-phase chunk: the MFMAs of chunk I (B operand b = the epilogue value of

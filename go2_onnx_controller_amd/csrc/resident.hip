@@ -49,6 +49,21 @@ constexpr int RES_GS = 4;    // GRU form: gate-fragment chunk slots per wave (I_
 
 typedef unsigned long long u64;
 
+// GO2PI_DIAG_RESCLK builds (tools/res_timeline.py): wall-clock (100 MHz) stamps of
+// one request's path through workgroup 0 (slots 0..15) and workgroup 17 (16..31,
+// another XCD), 32 per request, the last 512 requests (engine stamps buffer)
+#ifdef GO2PI_DIAG_RESCLK
+#define RES_STAMP(i)                                                                        \
+  do {                                                                                      \
+    if (P.stamps && tid == 0 && (g == 0 || g == 17))                                        \
+      P.stamps[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = wall_clock64();            \
+  } while (0)
+#else
+#define RES_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 // One wave sweeps n granules until every tag equals `tag`: 1 done, -1 a producer
 // left (GO2PI_RES_LEAVE tag), 0 timeout (err set).
 template <int SCOPE>
@@ -262,6 +277,8 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int in_dim = P.in_dim;
   unsigned last = 0;
+  unsigned nreq = 0;  // requests served by this launch (diagnostic stamps)
+  (void)nreq;
   // the batched-launch counter at launch (workgroup 0 leaves when it moves)
   const unsigned y0 =
       (g == 0 && yield) ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
@@ -352,6 +369,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         else
           wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
                                                   yield, y0);
+        RES_STAMP(0);
         const int n = (leave || CTL) ? 0 : B * in_dim;
         for (int i = lane; i < n; i += 64)
           __hip_atomic_store(mirror + 1 + i, ((u64)e << 32) | __float_as_uint(obsv[i]), __ATOMIC_RELAXED,
@@ -359,8 +377,10 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         if (lane == 0 && (leave || !CTL))
           __hip_atomic_store(mirror, leave ? ((u64)GO2PI_RES_LEAVE << 32) : (((u64)e << 32) | (unsigned)B),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        RES_STAMP(1);
       } else {
         wait_request<__HIP_MEMORY_SCOPE_AGENT>(mirror, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word);
+        RES_STAMP(0);
       }
       if (lane == 0) {
         st[0] = leave;
@@ -371,6 +391,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     }
     __syncthreads();
     if (st[0]) break;
+    RES_STAMP(2);
     const unsigned e = (unsigned)st[1];
     const int B = st[2];
     const unsigned word = (unsigned)st[3];
@@ -507,6 +528,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     }
     // ---- the layers (policy_latency_kernel's body; tags e + 1 + l)
     if constexpr (LOCAL0) local_layer0<NF>(P, w0, b0, obsv, x0, p0, xs, B, tid);
+    RES_STAMP(3);
     for (int l = LOCAL0 ? 1 : 0; l < P.nl; ++l) {
       const DevLayer &L = P.L[l];
       const int T = L.N_pad >> 4, C = L.K_pad >> 4, K_pad = L.K_pad;
@@ -540,6 +562,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         left = true;
         break;
       }
+      if (l < 6) RES_STAMP(2 * l + 2);  // layer l's input ready
       float p[GO2PI_SMALL_MAXB];
 #pragma unroll
       for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
@@ -602,8 +625,10 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         }
       }
       __syncthreads();  // xs / part reused by the next layer
+      if (l < 6) RES_STAMP(2 * l + 3);  // layer l published (the last: done written)
     }
     if (left) break;
+    ++nreq;
     if constexpr (RNN) {  // rows [0, B) now carry this request's h' (granules tagged e, in the other buffer)
       __syncthreads();     // every wave is done with lb for this request
       if (tid < B) {

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Batch-1 resident act() timeline (diagnostics): where a request's time goes.
+
+Needs a library whose resident kernel records wall-clock stamps
+(GO2PI_DIAG_RESCLK), built beside the default one:
+
+  cd go2_onnx_controller_amd/csrc && hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 \\
+      -I../../include -DGO2PI_DIAG_RESCLK -c resident.hip -o ../lib/diag/resident_clk.o && \\
+  hipcc -shared -fPIC --offload-arch=gfx950 -o ../lib/diag/libgo2pi_resclk.so ../lib/kernels.o \\
+      ../lib/kernels_w4_t2.o ../lib/kernels_w4_t4.o ../lib/kernels_w4_t8.o ../lib/diag/resident_clk.o \\
+      ../lib/engine.o ../lib/onnx_model.o
+
+  GO2PI_LIB=$PWD/go2_onnx_controller_amd/lib/diag/libgo2pi_resclk.so python3 tools/res_timeline.py
+
+Stamps (100 MHz wall clock, 10 ns) per request, relative to workgroup 0 seeing the
+request on the host: workgroup 0 (0 seen, 1 mirror stored, 2 waves released,
+3 layer 0 done, 2l+2 layer l input ready, 2l+3 layer l published / done written)
+and workgroup 17 (another XCD; same slots + 16). Host p50 beside them.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = {0: "seen", 1: "mirror stored", 2: "waves released", 3: "layer0 done"}
+for _l in range(1, 6):
+    NAMES[2 * _l + 2] = f"layer{_l} input ready"
+    NAMES[2 * _l + 3] = f"layer{_l} published"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="go2_mlp_512")
+    ap.add_argument("--iters", type=int, default=2000)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "res_timeline.json"))
+    args = ap.parse_args()
+    os.environ["GO2PI_DIAG_STAMPS"] = "1"
+    import numpy as np
+    from go2_onnx_controller_amd import Engine, synth
+    path = os.path.join(ROOT, "tests", "golden", "model.onnx") if args.model == "shipped" \
+        else synth.ensure_model(args.model)
+    with Engine(path, device=0, max_batch=4096, resident_ms=100) as e:
+        x = np.random.default_rng(2).standard_normal((1, e.in_dim)).astype(np.float32)
+        y = np.empty((1, e.out_dim), np.float32)
+        ts = []
+        for i in range(args.iters):
+            x[0, i % e.in_dim] += 1e-3
+            t0 = time.perf_counter_ns()
+            e.run_ptr(x.ctypes.data, y.ctypes.data, 1)
+            ts.append((time.perf_counter_ns() - t0) / 1e3)
+        st = e.diag_stamps(512 * 32).astype(np.int64).reshape(512, 32)  # syncs: waits for the idle exit
+    ts.sort()
+    rows = st[(st[:, 0] > 0) & (st[:, 9] > 0)]
+    base = rows[:, 0:1]
+    rel = (rows - base) * 10.0 / 1e3  # us
+    med = {}
+    for s in range(32):
+        col = rows[:, s]
+        ok = col > 0
+        if ok.sum() < len(rows) // 2:
+            continue
+        name = ("wg0 " if s < 16 else "wg17 ") + NAMES.get(s % 16, str(s % 16))
+        med[name] = round(float(np.median(rel[ok, s])), 3)
+    # the gap between a request's done and the next one's seen = host side + PCIe
+    gaps = (rows[1:, 0] - rows[:-1, 9]) * 10.0 / 1e3
+    out = {"model": args.model, "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2],
+           "host_p99_us": ts[int(len(ts) * 0.99)], "median_us_from_wg0_seen": med,
+           "median_done_to_next_seen_us": round(float(np.median(gaps)), 3)}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
