@@ -524,6 +524,15 @@ def main():
             p50, p99 = latency_b1(gru_path, local)
             out["latency_b1_gru_launch_p50_us"] = round(p50, 2)
             out["latency_b1_gru_launch_p99_us"] = round(p99, 2)
+            # LSTM-256 (the same head): resident (h as granules, c in the owning
+            # workgroups' LDS), then one fused launch per call
+            lstm_path = _synth.ensure_model("go2_lstm_256")
+            p50, p99 = latency_b1(lstm_path, local, resident_ms=100)
+            out["latency_b1_lstm_p50_us"] = round(p50, 2)
+            out["latency_b1_lstm_p99_us"] = round(p99, 2)
+            p50, p99 = latency_b1(lstm_path, local)
+            out["latency_b1_lstm_launch_p50_us"] = round(p50, 2)
+            out["latency_b1_lstm_launch_p99_us"] = round(p99, 2)
         if not args.no_gru and mname == "go2_mlp_512":
             out["gru256"] = gru_leg(local)
         if not args.no_ctl:

@@ -66,6 +66,12 @@ __device__ __forceinline__ void wg_barrier_vm() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for
+// its vector-memory ops. __syncthreads()'s fence also waits vmcnt(0), i.e. for
+// weight fragments just prefetched into registers (an L2 round trip on the
+// critical path of a batch-1 request's every layer) and for granule stores in flight.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void glds_copy(float *dst, const float *src, int n, int wave, int lane, int nw) {
   for (int base = wave * 64; base < n; base += nw * 64) {
     const int i = min(base + lane, n - 1);

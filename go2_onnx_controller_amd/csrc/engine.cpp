@@ -704,9 +704,10 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     const bool lat_shape = kmax <= 1024 && go2pi::latency_grid(p) <= 256 && e.small_batch > 0 &&
                            !std::getenv("GO2PI_SMALL_CHAIN");  // env: diagnostics, force the GEMV chain
     e.latency_ok = !m.has_gru && lat_shape;
-    // the resident kernel's GRU form (resident.hip, RNN): the cell tiled in front of
-    // the dense layers, h' carried between requests as granules
-    const bool res_rnn = m.has_gru && m.gru.cell == 0 && m.gru.lbr == 1 && m.gru.H % 64 == 0 &&
+    // the resident kernel's GRU / LSTM form (resident.hip, RNN): the cell tiled in front
+    // of the dense layers, h' carried between requests as granules (an LSTM's c in the
+    // owning workgroups' LDS)
+    const bool res_rnn = m.has_gru && ((m.gru.cell == 0 && m.gru.lbr == 1) || m.gru.cell == 1) && m.gru.H % 64 == 0 &&
                          p.gru.I_pad + m.gru.H <= 512 && (m.gru.H >> 4) <= 256 && lat_shape && e.opts.resident_ms > 0;
     e.palloc(&e.h_err, &e.m_err, 512);
     p.err = e.m_err + 64;  // batched kernel hand-off timeouts

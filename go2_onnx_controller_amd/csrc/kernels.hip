@@ -252,7 +252,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
       for (int b = 0; b < GO2PI_SMALL_MAXB; ++b)
         if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0 && lane < 16) {
       const int n = g * 16 + lane;
       const bool last = l == P.nl - 1;
@@ -279,7 +279,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
         }
       }
     }
-    __syncthreads();  // xs / part reused by the next layer
+    lds_barrier();  // xs / part reused by the next layer (the granule stores stay in flight)
   }
   if constexpr (CTL) {
     if (g != 0) return;

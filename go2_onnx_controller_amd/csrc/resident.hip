@@ -190,7 +190,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
     const int b = i / K0, k = i - b * K0;
     x0[i] = k < P.in_dim ? prologue(P, obsv[b * P.in_dim + k], k) : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
   const int n = tid % N0, ks = tid / N0;
   const int K1 = P.L[1].K_pad;  // layer 1's input row stride (= N0)
   for (int b = 0; b < B; ++b) {
@@ -212,7 +212,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
     }
   }
   if (KS > 1) {
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < B * N0; i += RES_WAVES * 64) {
       const int b = i / N0, nn = i - b * N0;
       float acc = 0.f;
@@ -220,7 +220,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
       xs[b * K1 + nn] = act_fn(L.act, L.alpha, acc + L.bias[nn]);
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 }  // namespace
@@ -233,11 +233,14 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
 // mirrors it, and post-processes the action into the staging (ctl_store); the
 // header's low word carries the batch and GO2PI_RES_* flags.
 //
-// RNN: a GRU policy (ONNX GRU, linear_before_reset = 1, H % 64 == 0). The cell
-// runs as a tiled layer in front of the dense ones: workgroup g < H / 16 owns
-// hidden units [16g, 16g + 16), its gate fragments held in registers for the
-// kernel's life; it computes z, r, n over [x | h] by GEMV (8 waves split the
-// k-chunks, fixed-order reductions) and publishes h' as {epoch, value} granules.
+// RNN: 1 a GRU policy (ONNX GRU, linear_before_reset = 1, H % 64 == 0), 2 an LSTM
+// policy (ONNX LSTM, gates i, o, f, c; no peepholes). The cell runs as a tiled
+// layer in front of the dense ones: workgroup g < H / 16 owns hidden units
+// [16g, 16g + 16), its gate fragments held in registers for the kernel's life; it
+// computes the gates over [x | h] by GEMV (8 waves split the k-chunks, fixed-order
+// reductions) and publishes h' as {epoch, value} granules. An LSTM's cell state
+// never leaves the workgroup that owns its units: it lives in that workgroup's LDS
+// between requests (first read from the engine's state rows, written back on leave).
 // Those granules ARE the carried hidden state: dense layer 0 sweeps them as its
 // input (tag = this request's epoch), and the next request's cell sweeps them as
 // its h (tag = the epoch of the last request that covered that row). Every
@@ -248,7 +251,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
 // them). A row not yet written in this launch comes from the engine's state rows
 // in HBM; each cell workgroup writes its units' latest h' back to those rows when
 // the kernel leaves (not while it runs: the rows are read then).
-template <int NF, bool CTL, bool RNN = false>
+template <int NF, bool CTL, int RNN = 0>
 __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
                                                                          const u64 *req, float *act, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
@@ -257,6 +260,8 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
                                                                          const unsigned *yield) {
   static_assert(!(RNN && (NF > 0 || CTL)), "the GRU form tiles layer 0 and serves act() only");
   constexpr bool LOCAL0 = NF > 0;
+  constexpr bool LSTM = RNN == 2;
+  constexpr int NG = LSTM ? 4 : 3;  // gate fragments per (chunk, tile)
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
   float *xs = reinterpret_cast<float *>(lds4);                       // [B][K_pad] layer input
@@ -284,15 +289,17 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       (g == 0 && yield) ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   // RNN: the cell's LDS (after the CTL regions: RNN and CTL are exclusive)
   const int Hh = RNN ? P.gru.H : 0, Ip = RNN ? P.gru.I_pad : 0, Kg = Ip + Hh, Cg = Kg >> 4, Cx = Ip >> 4;
+  const int SW = RNN ? P.gru.sw : 0;  // state floats per robot row (LSTM: h | c)
   const int Ht = Hh >> 4;
   float *hx = cbase;                                      // [B][Kg] the cell's input rows [x | h]
   float *hpart = hx + GO2PI_SMALL_MAXB * Kg;              // [waves][4][B][16] partial sums (z, r, n_x, n_h)
   unsigned *le = reinterpret_cast<unsigned *>(hpart + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16);  // [B] row epochs
   unsigned *lb = le + GO2PI_SMALL_MAXB;                   // [B] the granule buffer holding each row's h
   float *hown = reinterpret_cast<float *>(lb + GO2PI_SMALL_MAXB);  // [B][16] this workgroup's units' latest h'
+  float *cown = hown + GO2PI_SMALL_MAXB * 16;             // LSTM: [B][16] its units' cell state
   const size_t hbuf = (size_t)GO2PI_SMALL_MAXB * Hh;      // granules per buffer
-  float4 wgf[RES_GS][3];                                  // this workgroup's gate fragments (chunks wave + 8s)
-  float gb[4] = {0.f, 0.f, 0.f, 0.f};                     // its biases: z, r (summed), Wb_h, Rb_h
+  float4 wgf[RES_GS][NG];                                 // this workgroup's gate fragments (chunks wave + 8s)
+  float gb[4] = {0.f, 0.f, 0.f, 0.f};                     // its biases: GRU z, r (summed), Wb_h, Rb_h; LSTM i, o, f, c
   if constexpr (RNN) {
     if (tid < GO2PI_SMALL_MAXB) le[tid] = lb[tid] = 0u;
     if (g < Ht) {
@@ -301,15 +308,20 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       for (int s = 0; s < RES_GS; ++s) {
         const int c = wave + s * RES_WAVES;
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          wgf[s][q] = c < Cg ? Wg[(((size_t)c * Ht + g) * 3 + q) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < NG; ++q)
+          wgf[s][q] = c < Cg ? Wg[(((size_t)c * Ht + g) * NG + q) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       if (wave == 0 && lane < 16) {
         const int j = g * 16 + lane;
-        gb[0] = P.gru.bzr[j];
-        gb[1] = P.gru.bzr[Hh + j];
-        gb[2] = P.gru.bh[j];
-        gb[3] = P.gru.bh[Hh + j];
+        if constexpr (LSTM) {  // Wb + Rb per gate, summed at load
+#pragma unroll
+          for (int q = 0; q < 4; ++q) gb[q] = P.gru.bzr[q * Hh + j];
+        } else {
+          gb[0] = P.gru.bzr[j];
+          gb[1] = P.gru.bzr[Hh + j];
+          gb[2] = P.gru.bh[j];
+          gb[3] = P.gru.bh[Hh + j];
+        }
       }
     }
   }
@@ -389,7 +401,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         st[3] = (int)word;
       }
     }
-    __syncthreads();
+    lds_barrier();  // (the mirror stores stay in flight)
     if (st[0]) break;
     RES_STAMP(2);
     const unsigned e = (unsigned)st[1];
@@ -397,6 +409,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     const unsigned word = (unsigned)st[3];
     last = e;
     bool left = false;
+    bool refill = false;  // this workgroup's last layer ran: its first layer's fragments are due
     CtlView cv{};
     if constexpr (CTL) {
       if (g == 0) {
@@ -445,7 +458,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
                 lane == 0)
               st[0] = 1;
           } else {
-            for (int k = lane; k < Hh; k += 64) hx[b * Kg + Ip + k] = hidden[(size_t)b * Hh + k];
+            for (int k = lane; k < Hh; k += 64) hx[b * Kg + Ip + k] = hidden[(size_t)b * SW + k];
           }
         }
         __syncthreads();
@@ -473,10 +486,15 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
             for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
               if (b < B) {
                 const float4 a = *reinterpret_cast<const float4 *>(hx + b * Kg + c * 16 + koff);
-                pz[b] = dot4(a, wgf[s][0], pz[b]);
+                pz[b] = dot4(a, wgf[s][0], pz[b]);  // LSTM: i, o, f, c in pz, pr, pnx, pnh
                 pr[b] = dot4(a, wgf[s][1], pr[b]);
-                if (xc) pnx[b] = dot4(a, wgf[s][2], pnx[b]);
-                else pnh[b] = dot4(a, wgf[s][2], pnh[b]);
+                if constexpr (LSTM) {
+                  pnx[b] = dot4(a, wgf[s][2], pnx[b]);
+                  pnh[b] = dot4(a, wgf[s][NG - 1], pnh[b]);
+                } else {
+                  if (xc) pnx[b] = dot4(a, wgf[s][2], pnx[b]);
+                  else pnh[b] = dot4(a, wgf[s][2], pnh[b]);
+                }
               }
             }
           }
@@ -514,9 +532,20 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
                 for (int w2 = 0; w2 < RES_WAVES; ++w2) a += hpart[((w2 * 4 + k) * GO2PI_SMALL_MAXB + b) * 16 + lane];
                 q[k] = a + gb[k];
               }
-              const float zg = sigmoid_fast(q[0]), rg = sigmoid_fast(q[1]);
-              const float hv = 2.f * sigmoid_fast(2.f * (q[2] + rg * q[3])) - 1.f;  // tanh, ~1e-7 abs
-              const float hnew = (1.f - zg) * hv + zg * hx[b * Kg + Ip + j];
+              float hnew;
+              if constexpr (LSTM) {  // the gate math of lstm_group (fused_impl.hpp)
+                const float ig = sigmoid_fast(q[0]), og = sigmoid_fast(q[1]), fg = sigmoid_fast(q[2]);
+                const float cg = 2.f * sigmoid_fast(2.f * q[3]) - 1.f;  // tanh, ~1e-7 abs
+                // c: this workgroup's LDS copy once the row ran in this launch, else the state row
+                const float c_old = le[b] != 0u ? cown[b * 16 + lane] : hidden[(size_t)b * SW + Hh + j];
+                const float c_new = fg * c_old + ig * cg;
+                cown[b * 16 + lane] = c_new;
+                hnew = og * (2.f * sigmoid_fast(2.f * c_new) - 1.f);
+              } else {
+                const float zg = sigmoid_fast(q[0]), rg = sigmoid_fast(q[1]);
+                const float hv = 2.f * sigmoid_fast(2.f * (q[2] + rg * q[3])) - 1.f;  // tanh, ~1e-7 abs
+                hnew = (1.f - zg) * hv + zg * hx[b * Kg + Ip + j];
+              }
               hown[b * 16 + lane] = hnew;
               __hip_atomic_store(hgran + (1u - lb[b]) * hbuf + (size_t)b * Hh + j, ((u64)e << 32) | __float_as_uint(hnew),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -562,7 +591,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         left = true;
         break;
       }
-      if (l < 6) RES_STAMP(2 * l + 2);  // layer l's input ready
+      if (l < 5) RES_STAMP(2 * l + 2);  // layer l's input ready
       float p[GO2PI_SMALL_MAXB];
 #pragma unroll
       for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) p[b] = 0.f;
@@ -592,12 +621,15 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         for (int b = 0; b < GO2PI_SMALL_MAXB; ++b)
           if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
       }
+      if (l == 1) RES_STAMP(12);  // layer 1: partial sums written
       const float bcur = bv;
-      {
-        const int ln = owned_from(l + 1);  // the next owned layer, else the first of the next request
-        load_layer(ln < P.nl ? ln : l_first);
-      }
-      __syncthreads();
+      // the next owned layer's fragments, in flight across the barriers and the next
+      // hand-off; after this workgroup's last layer, the next request's first layer
+      // is fetched once the request is answered (not in front of the action's drain)
+      const int ln = owned_from(l + 1);
+      if (ln < P.nl) load_layer(ln);
+      lds_barrier();
+      if (l == 1) RES_STAMP(13);  // layer 1: partials visible
       if (wave == 0 && lane < 16) {
         const int n = g * 16 + lane;
         const bool lastl = l == P.nl - 1;
@@ -624,11 +656,12 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           }
         }
       }
-      __syncthreads();  // xs / part reused by the next layer
-      if (l < 6) RES_STAMP(2 * l + 3);  // layer l published (the last: done written)
+      if (l == 1) RES_STAMP(14);  // layer 1: wave 0's granules stored
+      lds_barrier();  // xs / part reused by the next layer
+      if (l < 5) RES_STAMP(2 * l + 3);  // layer l published (the last: done written)
+      if (ln >= P.nl) refill = true;
     }
     if (left) break;
-    ++nreq;
     if constexpr (RNN) {  // rows [0, B) now carry this request's h' (granules tagged e, in the other buffer)
       __syncthreads();     // every wave is done with lb for this request
       if (tid < B) {
@@ -646,13 +679,19 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         if (tid == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
+    // the next request's first-layer fragments, after this one is answered (they
+    // land while the next request is awaited)
+    if (refill && l_first < P.nl) load_layer(l_first);
+    ++nreq;
   }
   // ---- leave: consumers still waiting on this workgroup's slots leave too
   tag_leave(P, gran, gstride, g, tid, LOCAL0 ? 1 : 0, RNN ? hgran : nullptr);
   if constexpr (RNN) {  // the rows this launch advanced go back to the engine's state rows
     __syncthreads();
-    if (g < Ht && tid < GO2PI_SMALL_MAXB * 16 && le[tid >> 4] != 0u)
-      hidden[(size_t)(tid >> 4) * Hh + g * 16 + (tid & 15)] = hown[tid];
+    if (g < Ht && tid < GO2PI_SMALL_MAXB * 16 && le[tid >> 4] != 0u) {
+      hidden[(size_t)(tid >> 4) * SW + g * 16 + (tid & 15)] = hown[tid];
+      if constexpr (LSTM) hidden[(size_t)(tid >> 4) * SW + Hh + g * 16 + (tid & 15)] = cown[tid];
+    }
   }
   if (g == 0 && tid == 0)
     __hip_atomic_store(mirror, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -670,8 +709,9 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   for (int l = 0; l < p.nl; ++l)
     if (p.L[l].K_pad > RES_MAXS * RES_WAVES * 16) return (int)hipErrorInvalidValue;
   const bool rnn = p.has_gru != 0;
-  if (rnn && (ctl || p.gru.cell != 0 || p.gru.lbr != 1 || p.gru.H % 64 || p.gru.I_pad + p.gru.H > RES_GS * RES_WAVES * 16 ||
-              !hgran || !hidden))
+  const bool lstm = rnn && p.gru.cell == 1;
+  if (rnn && (ctl || p.gru.cell > 1 || (!lstm && p.gru.lbr != 1) || p.gru.H % 64 ||
+              p.gru.I_pad + p.gru.H > RES_GS * RES_WAVES * 16 || !hgran || !hidden))
     return (int)hipErrorInvalidValue;
   // local layer 0 where each thread's share of it fits NF = 8, 12 or 16 registers'
   // fragments (a slice's chunks past layer 0's own are zero fragments on zero columns)
@@ -692,7 +732,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   if (ctl) tail = (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
   if (rnn)
     tail = (size_t)GO2PI_SMALL_MAXB * (p.gru.I_pad + p.gru.H) + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16 +
-           2 * GO2PI_SMALL_MAXB + GO2PI_SMALL_MAXB * 16;
+           2 * GO2PI_SMALL_MAXB + GO2PI_SMALL_MAXB * 16 * (lstm ? 2 : 1);
   const size_t lds = sizeof(float) * (ctl_off + tail);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {
@@ -705,7 +745,8 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
                        act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden, yield);
     return (int)hipGetLastError();
   };
-  if (rnn) return go(policy_resident_kernel<0, false, true>);
+  if (lstm) return go(policy_resident_kernel<0, false, 2>);
+  if (rnn) return go(policy_resident_kernel<0, false, 1>);
   if (ctl) {
     if (local0 && nf == 8) return go(policy_resident_kernel<8, true>);
     if (local0 && nf == 12) return go(policy_resident_kernel<12, true>);

@@ -302,6 +302,68 @@ def test_resident_gru_idle_exit_keeps_state(synth_path):
             time.sleep(float(rng.uniform(0.0, 0.008)))
 
 
+def _lstm_oracle_step(path, x, hc):
+    from oracle import onnx_ref
+    g = onnx_ref.load(path)
+    H = hc.shape[1] // 2
+    r = onnx_ref.run(g, {"observation": x.astype(np.float64), "h_in": hc[None, :, :H], "c_in": hc[None, :, H:]})
+    return r["action"], np.concatenate([r["h_out"][0], r["c_out"][0]], axis=1)
+
+
+@pytest.mark.parametrize("name", ["go2_lstm_256", "lstm_128"])
+def test_resident_lstm_rollout(synth_path, name):
+    """The resident kernel's LSTM form (resident.hip, RNN = 2): h' carried between
+    requests as tagged granules, the cell state c in the owning workgroups' LDS.
+    40 requests at batch 1..8 with a masked reset, a set_hidden and get_hidden reads
+    (h | c rows) interleaved, against the fp64 ONNX-LSTM oracle rollout per row and
+    against the launch-per-call engine."""
+    from go2_onnx_controller_amd import Engine
+    p = synth_path(name)
+    rng = np.random.default_rng(29)
+    with Engine(p, max_batch=8, resident_ms=500) as r, Engine(p, max_batch=8) as q:
+        S = r.hidden_dim  # 2H: h | c
+        hc_ref = np.zeros((8, S))
+        r.reset_hidden()
+        q.reset_hidden()
+        for i in range(40):
+            B = [1, 1, 2, 8, 3, 1, 5, 8][i % 8]
+            x = rng.standard_normal((B, r.in_dim)).astype(np.float32)
+            want, hc_new = _lstm_oracle_step(p, x, hc_ref[:B])
+            hc_ref[:B] = hc_new
+            assert abs_err(r.run(x), want) <= TOL, f"request {i} B={B}"
+            assert abs_err(q.run(x), want) <= TOL, f"request {i} B={B} (launch path)"
+            if i == 12:
+                mask = np.array([0, 1, 1, 0, 1, 0, 0, 0], np.uint8)
+                r.reset_hidden(mask)
+                q.reset_hidden(mask)
+                hc_ref[mask == 1] = 0
+            if i == 25:
+                s = rng.standard_normal((8, S)).astype(np.float32) * 0.5
+                r.set_hidden(s)
+                q.set_hidden(s)
+                hc_ref[:] = s
+            if i % 10 == 9:
+                assert abs_err(r.get_hidden(8), hc_ref) <= TOL, f"request {i}: h | c rows"
+
+
+def test_resident_lstm_idle_exit_keeps_state(synth_path):
+    """resident_ms = 3: the LSTM kernel leaves between requests; its h and c
+    write-back to the state rows carries both across relaunches."""
+    from go2_onnx_controller_amd import Engine
+    p = synth_path("lstm_128")
+    rng = np.random.default_rng(31)
+    with Engine(p, max_batch=8, resident_ms=3) as r:
+        hc_ref = np.zeros((8, r.hidden_dim))
+        for i in range(30):
+            B = 1 + i % 3
+            x = rng.standard_normal((B, r.in_dim)).astype(np.float32)
+            want, hc_new = _lstm_oracle_step(p, x, hc_ref[:B])
+            hc_ref[:B] = hc_new
+            assert abs_err(r.run(x), want) <= TOL, f"request {i}"
+            time.sleep(float(rng.uniform(0.0, 0.008)))
+        assert abs_err(r.get_hidden(8), hc_ref) <= TOL
+
+
 def test_batched_launch_evicts_other_resident_kernels(synth_path):
     """A batched launch on the device tells other engines' live resident kernels to
     leave (they hold CUs the launch needs: DESIGN §4.2b); the evicted engine's act()

@@ -26,8 +26,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = {0: "seen", 1: "mirror stored", 2: "waves released", 3: "layer0 done"}
-for _l in range(1, 6):
+NAMES = {0: "seen", 1: "mirror stored", 2: "waves released", 3: "layer0 done", 12: "layer1 partials written",
+         13: "layer1 partials visible", 14: "layer1 wave0 stored"}
+for _l in range(1, 5):
     NAMES[2 * _l + 2] = f"layer{_l} input ready"
     NAMES[2 * _l + 3] = f"layer{_l} published"
 
