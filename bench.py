@@ -151,6 +151,28 @@ def latency_b1(model_path, device, iters=10000, warm=1000, resident_ms=0):
     return _pct(ts, 0.5), _pct(ts, 0.99)
 
 
+def latency_b1_cpp(model_path, in_dim, out_dim, iters=10000, warm=1000):
+    """p50/p99 of ONNXActor::act() at batch 1 timed in C++ the way the reference's
+    own driver times it (onnx_inference/src/cpp/main.cpp:38-42: steady_clock around
+    one act()), through the drop-in shim (libonnx_actor.so, resident kernel by
+    default): tests/cpp/controller_shape.cpp's `lat` mode, built here with g++ if
+    absent. None when it cannot be built or run."""
+    lib = os.path.join(ROOT, "go2_onnx_controller_amd", "lib")
+    exe = os.path.join(ROOT, "build", "controller_shape")
+    src = os.path.join(ROOT, "tests", "cpp", "controller_shape.cpp")
+    try:
+        if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+            os.makedirs(os.path.dirname(exe), exist_ok=True)
+            subprocess.run(["g++", "-std=c++20", "-O2", "-I" + os.path.join(ROOT, "include"), src, "-L" + lib,
+                            "-lonnx_actor", "-Wl,-rpath," + lib, "-o", exe], check=True, capture_output=True)
+        r = subprocess.run([exe, model_path, "lat", str(iters), str(warm), str(in_dim), str(out_dim)],
+                           capture_output=True, text=True, timeout=120)
+        vals = dict(ln.split(": ") for ln in r.stdout.splitlines() if ln.startswith("p"))
+        return float(vals["p50_us"]), float(vals["p99_us"])
+    except (OSError, subprocess.SubprocessError, KeyError, ValueError):
+        return None
+
+
 def timed_launches(call, stream, dev, n, warm):
     """Average microseconds per `call` from HIP events recorded on `stream` (the stream
     the kernels are launched on)."""
@@ -397,7 +419,7 @@ def main():
         model_path = os.path.join(ROOT, "tests", "golden", "model.onnx") if mname == "__shipped__" \
             else synth.ensure_model(mname)
         eng = Engine(model_path, device=local, max_batch=batch, waves=args.waves)
-        in_dim = eng.in_dim
+        in_dim, out_dim = eng.in_dim, eng.out_dim
         gen = torch.Generator(device="cpu").manual_seed(1 + rank)
         obs = torch.randn((ticks, batch, eng.in_dim), generator=gen).to(dev)
         act = torch.empty((ticks, batch, eng.out_dim), device=dev)
@@ -514,6 +536,19 @@ def main():
             p50, p99 = latency_b1(model_path, local)
             out["latency_b1_launch_p50_us"] = round(p50, 2)
             out["latency_b1_launch_p99_us"] = round(p99, 2)
+            # the same act() timed from C++ through the drop-in ONNXActor, as the
+            # reference's main.cpp times it (the legs above call through Python ctypes)
+            shipped = os.path.join(ROOT, "tests", "golden", "model.onnx")
+            cpp = {}
+            for name, path, i_d, o_d in (("go2_mlp_512", model_path, in_dim, out_dim),
+                                         ("shipped", shipped, 98, 12)):
+                r = latency_b1_cpp(path, i_d, o_d)
+                if r:
+                    cpp[name] = {"p50_us": round(r[0], 2), "p99_us": round(r[1], 2)}
+            if cpp:
+                cpp["what"] = ("ONNXActor::act() at batch 1 timed in C++ (steady_clock around one call, "
+                               "main.cpp:38-42), resident kernel, 1,000 warm + 10,000 timed calls")
+                out["latency_b1_act_cpp"] = cpp
             # the recurrent policy (configs[4]'s GRU-256) at batch 1: the resident kernel's GRU
             # form (hidden rows carried inside the live kernel), then one fused launch per call
             from go2_onnx_controller_amd import synth as _synth

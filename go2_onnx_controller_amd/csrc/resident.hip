@@ -58,8 +58,17 @@ typedef unsigned long long u64;
     if (P.stamps && tid == 0 && (g == 0 || g == 17))                                        \
       P.stamps[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = wall_clock64();            \
   } while (0)
+// shader-clock stamp beside them (slot i): the clock the request ran at
+#define RES_CLOCK(i)                                                                        \
+  do {                                                                                      \
+    if (P.stamps && tid == 0 && (g == 0 || g == 17))                                        \
+      P.stamps[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define RES_STAMP(i) \
+  do {               \
+  } while (0)
+#define RES_CLOCK(i) \
   do {               \
   } while (0)
 #endif
@@ -404,6 +413,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     lds_barrier();  // (the mirror stores stay in flight)
     if (st[0]) break;
     RES_STAMP(2);
+    RES_CLOCK(15);
     const unsigned e = (unsigned)st[1];
     const int B = st[2];
     const unsigned word = (unsigned)st[3];
@@ -611,10 +621,15 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           }
         }
       }
+      if (l == 1) RES_STAMP(10);  // layer 1: fma chains done
+      // the four 16-lane row groups' partials summed (rows past the request's batch skipped:
+      // each cross-lane step is an LDS-latency permute)
 #pragma unroll
       for (int b = 0; b < GO2PI_SMALL_MAXB; ++b) {
-        p[b] += __shfl_xor(p[b], 16);
-        p[b] += __shfl_xor(p[b], 32);
+        if (b < B) {
+          p[b] += __shfl_xor(p[b], 16);
+          p[b] += __shfl_xor(p[b], 32);
+        }
       }
       if (lane < 16) {
 #pragma unroll
@@ -659,6 +674,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       if (l == 1) RES_STAMP(14);  // layer 1: wave 0's granules stored
       lds_barrier();  // xs / part reused by the next layer
       if (l < 5) RES_STAMP(2 * l + 3);  // layer l published (the last: done written)
+      if (l == 2) RES_CLOCK(11);
       if (ln >= P.nl) refill = true;
     }
     if (left) break;

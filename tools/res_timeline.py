@@ -26,9 +26,10 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = {0: "seen", 1: "mirror stored", 2: "waves released", 3: "layer0 done", 12: "layer1 partials written",
+NAMES = {0: "seen", 1: "mirror stored", 2: "waves released", 3: "layer0 done", 10: "layer1 fma done",
+         12: "layer1 partials written",
          13: "layer1 partials visible", 14: "layer1 wave0 stored"}
-for _l in range(1, 5):
+for _l in range(1, 4):
     NAMES[2 * _l + 2] = f"layer{_l} input ready"
     NAMES[2 * _l + 3] = f"layer{_l} published"
 
@@ -64,13 +65,21 @@ def main():
         ok = col > 0
         if ok.sum() < len(rows) // 2:
             continue
+        if s % 16 in (11, 15):  # shader-clock stamps, not wall clock
+            continue
         name = ("wg0 " if s < 16 else "wg17 ") + NAMES.get(s % 16, str(s % 16))
         med[name] = round(float(np.median(rel[ok, s])), 3)
+    # shader clock over waves released -> layer 2 published (slots 15 / 11: s_memtime)
+    dt_us = (rows[:, 7] - rows[:, 2]) * 10.0 / 1e3
+    ghz = (rows[:, 11] - rows[:, 15]) / np.maximum(dt_us, 1e-3) / 1e3
+    med.pop("wg0 15", None)
+    med.pop("wg0 11", None)
     # the gap between a request's done and the next one's seen = host side + PCIe
     gaps = (rows[1:, 0] - rows[:-1, 9]) * 10.0 / 1e3
     out = {"model": args.model, "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2],
            "host_p99_us": ts[int(len(ts) * 0.99)], "median_us_from_wg0_seen": med,
-           "median_done_to_next_seen_us": round(float(np.median(gaps)), 3)}
+           "median_done_to_next_seen_us": round(float(np.median(gaps)), 3),
+           "shader_clock_ghz_median": round(float(np.median(ghz)), 3)}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump(out, fh, indent=1)
