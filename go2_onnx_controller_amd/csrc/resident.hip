@@ -46,6 +46,11 @@ constexpr int RES_WAVES = 8;
 constexpr int RES_MAXS = 8;  // chunk slots per wave held in registers (K_pad <= 1024)
 constexpr int RES_POLL = 2;  // header + observation granules per lane in the idle poll (<= 127 obs floats)
 constexpr int RES_GS = 4;    // GRU form: gate-fragment chunk slots per wave (I_pad + H <= 512)
+// The wave that sums a layer's partials and publishes its granules (and an RNN
+// cell's h'): the last one, not wave 0, which alone sweeps the next layer's input
+// at batch 1 (a wave's loads complete in order behind its own stores, so a
+// publishing sweeper waits for its granule stores to be acknowledged first)
+constexpr int RES_PW = RES_WAVES - 1;
 
 typedef unsigned long long u64;
 
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         for (int q = 0; q < NG; ++q)
           wgf[s][q] = c < Cg ? Wg[(((size_t)c * Ht + g) * NG + q) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      if (wave == 0 && lane < 16) {
+      if (wave == RES_PW && lane < 16) {
         const int j = g * 16 + lane;
         if constexpr (LSTM) {  // Wb + Rb per gate, summed at load
 #pragma unroll
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       const int c = wave + s * RES_WAVES;
       wr[s] = c < C ? W[(size_t)c * T * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
+    bv = (wave == RES_PW && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
   };
   const int l_first = owned_from(0);
   if (l_first < P.nl) load_layer(l_first);
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
             }
           }
           __syncthreads();
-          if (wave == 0 && lane < 16) {
+          if (wave == RES_PW && lane < 16) {
             const int j = g * 16 + lane;
             for (int b = 0; b < B; ++b) {
               float q[4];
@@ -645,7 +650,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       if (ln < P.nl) load_layer(ln);
       lds_barrier();
       if (l == 1) RES_STAMP(13);  // layer 1: partials visible
-      if (wave == 0 && lane < 16) {
+      if (wave == RES_PW && lane < 16) {
         const int n = g * 16 + lane;
         const bool lastl = l == P.nl - 1;
         for (int b = 0; b < B; ++b) {
@@ -697,7 +702,13 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     }
     // the next request's first-layer fragments, after this one is answered (they
     // land while the next request is awaited)
-    if (refill && l_first < P.nl) load_layer(l_first);
+    if (refill && l_first < P.nl) {
+      load_layer(l_first);
+      // drained here, in the idle time before the next request (the builtin, unlike an
+      // asm wait, tells the compiler's waitcnt pass: the next request's first use of
+      // these registers then waits for nothing, not for every store issued since)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
     ++nreq;
   }
   // ---- leave: consumers still waiting on this workgroup's slots leave too
