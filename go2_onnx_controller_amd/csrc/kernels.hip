@@ -130,6 +130,9 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
 // match. Spins are bounded: on timeout the workgroup writes `err` and stops.
 constexpr int LAT_WAVES = 8;
 constexpr int LAT_MAXS = 8;  // chunk slots per wave held in registers (K_pad <= 1024)
+// the wave that sums a layer's partials and publishes it: the last one, since wave 0
+// alone sweeps a batch-1 layer input (its loads would complete behind its own stores)
+constexpr int LAT_PW = LAT_WAVES - 1;
 
 __device__ __forceinline__ bool sweep_layer(unsigned long long *gran, int n, unsigned tag, float *dst,
                                             unsigned *err, int lane) {
@@ -200,7 +203,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
       const int c = wave + s * LAT_WAVES;
       wr[s] = c < C ? W[(size_t)c * T * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float bv = (wave == 0 && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
+    const float bv = (wave == LAT_PW && lane < 16) ? L.bias[g * 16 + lane] : 0.f;
     if (l == 0) {
       const float *src = obs;
       if constexpr (CTL) {
@@ -253,7 +256,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
         if (b < B) part[(wave * GO2PI_SMALL_MAXB + b) * 16 + lane] = p[b];
     }
     lds_barrier();
-    if (wave == 0 && lane < 16) {
+    if (wave == LAT_PW && lane < 16) {
       const int n = g * 16 + lane;
       const bool last = l == P.nl - 1;
       for (int b = 0; b < B; ++b) {
