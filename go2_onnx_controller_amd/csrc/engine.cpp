@@ -124,6 +124,7 @@ struct go2pi_engine {
   int tmp_stride = 0;
   float *h_obs = nullptr, *h_act = nullptr;  // pinned, host-mapped
   float *m_obs = nullptr, *m_act = nullptr;  // device aliases of the above
+  unsigned long long *h_actg = nullptr, *m_actg = nullptr;  // resident act(): {epoch, value} action granules
   hipGraphExec_t graphs[GO2PI_SMALL_MAXB + 1] = {};
   hipGraph_t graph_defs[GO2PI_SMALL_MAXB + 1] = {};
   go2pi_cost cost{};
@@ -261,7 +262,8 @@ struct go2pi_engine {
                 "hipMemsetAsync");
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
-    hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_act, d_gran, gstride, d_mirror, m_err, m_done,
+    std::memset(h_actg, 0, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)model.out_dim);
+    hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,
                                      res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
               "resident launch");
     resident_live = true;
@@ -303,9 +305,28 @@ struct go2pi_engine {
       __atomic_store_n(h_req, ((unsigned long long)e0 << 32) | (unsigned)batch | flags, __ATOMIC_RELEASE);
       const auto t0 = std::chrono::steady_clock::now();
       unsigned d;
-      for (unsigned it = 0; (d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) != e0 && d != GO2PI_RES_LEAVE; ++it) {
-        __builtin_ia32_pause();
-        if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+      if (ctl) {  // the controller form: a done word behind the drained outputs
+        for (unsigned it = 0; (d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) != e0 && d != GO2PI_RES_LEAVE; ++it) {
+          __builtin_ia32_pause();
+          if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+        }
+      } else {  // act(): the action granules themselves, every tag = this request's epoch
+        const int nout = (int)batch * model.out_dim;
+        for (unsigned it = 0;; ++it) {
+          int i = 0;
+          while (i < nout && (unsigned)(__atomic_load_n(h_actg + i, __ATOMIC_RELAXED) >> 32) == e0) ++i;
+          if (i == nout) {
+            d = e0;
+            for (int j = 0; j < nout; ++j) {
+              const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
+              std::memcpy(h_act + j, &bits, 4);
+            }
+            break;
+          }
+          if ((d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) == GO2PI_RES_LEAVE) break;
+          __builtin_ia32_pause();
+          if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+        }
       }
       res_last = std::chrono::steady_clock::now();
       if (d == e0) return true;
@@ -726,6 +747,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       // room for a controller tick's rows too (GO2PI_CTL_RAW + in_dim floats per robot)
       const size_t nreq = 1 + GO2PI_SMALL_MAXB * (size_t)(m.in_dim + GO2PI_CTL_RAW);
       e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
+      e.palloc(&e.h_actg, &e.m_actg, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)m.out_dim);
       e.d_mirror = e.dalloc<unsigned long long>(1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim);
       int khz = 0;
       hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.device), "hipDeviceGetAttribute");

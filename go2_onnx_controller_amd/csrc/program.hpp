@@ -182,7 +182,11 @@ int launch_latency_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCt
 // tiled layer: hgran = device [2][SMALL_MAXB][H] granules (zeroed before every
 // launch) carry h' between requests, hidden = the engine's state rows (read for
 // rows not yet written in this launch, written back when the kernel leaves).
-int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
+// act() form: the action rows travel to the host as {epoch, value} granules in actg
+// (host-mapped [SMALL_MAXB][out_dim]): the host checks the data itself, so no drain
+// and no done word sit between the last store and the answer.
+int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
+                    unsigned long long *actg,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
                     float *hidden, const unsigned *yield, void *stream);

@@ -267,7 +267,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
 // the kernel leaves (not while it runs: the rows are read then).
 template <int NF, bool CTL, int RNN = 0>
 __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const DevProgram *__restrict__ Pd,
-                                                                         const u64 *req, float *act, u64 *gran,
+                                                                         const u64 *req, u64 *actg, u64 *gran,
                                                                          int gstride, u64 *mirror, unsigned *err,
                                                                          unsigned *done, u64 idle_ticks, DevCtl C,
                                                                          u64 *hgran, float *hidden,
@@ -377,6 +377,10 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
     }
     b0 = L.bias[n];
   }
+  // every fragment held across requests has landed before the first wait (and the
+  // compiler's waitcnt pass knows it: no vmcnt(0) in front of their first uses,
+  // which would also wait for the stores a request has in flight by then)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
   for (;;) {
     // ---- wait for a request. Workgroup 0 polls the host (header + the first
@@ -660,14 +664,11 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
           if (lastl) {
             if constexpr (CTL) {
               if (n < L.N) ctl_store(cv, b, n, post_fn(P, v));
-            } else {
-              if (n < L.N) act[(size_t)b * L.N + n] = post_fn(P, v);
-            }
-            if (!CTL && b == B - 1 && g == 0) {
-              // every action store of this tile drained and system-visible before the done word
-              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              if (lane == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else if (n < L.N) {
+              // the action as {epoch, value} granules in host memory: the host's spin reads
+              // the data itself (no release drain, no done word behind it)
+              __hip_atomic_store(actg + (size_t)b * L.N + n, ((u64)e << 32) | __float_as_uint(post_fn(P, v)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
           } else {
             const u64 gv = ((u64)(e + 1u + (unsigned)l) << 32) | __float_as_uint(v);
@@ -728,7 +729,8 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   }
 }
 
-int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req, float *act,
+int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
+                    unsigned long long *actg,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
                     float *hidden, const unsigned *yield, void *stream) {
@@ -769,7 +771,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
       if (a != hipSuccess) return (int)a;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(RES_WAVES * 64), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req,
-                       act, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden, yield);
+                       actg, gran, gstride, mirror, err, done, idle_ticks, ctl ? *ctl : DevCtl{}, hgran, hidden, yield);
     return (int)hipGetLastError();
   };
   if (lstm) return go(policy_resident_kernel<0, false, 2>);
