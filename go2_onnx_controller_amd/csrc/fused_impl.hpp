@@ -1530,7 +1530,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
       if (sub) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 46 + wave] = __builtin_amdgcn_s_memtime();
 #endif
-      if constexpr (HO) {
+      if constexpr (HO && PL) {
+        // the lean kernel publishes after its first own chunk: the publish's
+        // lgkmcnt(0) then finds the tile stores landed instead of holding the MFMAs
+        // behind them (mlp512 35.55 -> 35.43 us median, profiles/r03_ab_latepub.json;
+        // the GRU body measured no gain: 60.05 vs 60.16 us, so it keeps the early flag)
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          ((w4_chunk<TPW, (I & 3), RD, true, true>(accn, f, v[I], ws, vo, ((t0 + I + RD) & (CH - 1)) * CSB),
+            I == 0 ? publish() : void()),
+           ...);
+        }(std::make_integer_sequence<int, TPW>{});
+      } else if constexpr (HO) {
         publish();
         [&]<int... I>(std::integer_sequence<int, I...>) {
           (w4_chunk<TPW, (I & 3), RD, true, true>(accn, f, v[I], ws, vo, ((t0 + I + RD) & (CH - 1)) * CSB), ...);
