@@ -1530,7 +1530,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
       if (sub) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 46 + wave] = __builtin_amdgcn_s_memtime();
 #endif
-      if constexpr (HO && PL) {
+#ifdef GO2PI_DIAG_LATEPUBALL  // variant (diagnostics): the late flag in the general body too
+      constexpr bool LATEPUB = HO;
+#else
+      constexpr bool LATEPUB = HO && PL;
+#endif
+      if constexpr (LATEPUB) {
         // the lean kernel publishes after its first own chunk: the publish's
         // lgkmcnt(0) then finds the tile stores landed instead of holding the MFMAs
         // behind them (mlp512 35.55 -> 35.43 us median, profiles/r03_ab_latepub.json;
