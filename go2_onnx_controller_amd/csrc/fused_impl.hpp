@@ -1539,7 +1539,8 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
         // the lean kernel publishes after its first own chunk: the publish's
         // lgkmcnt(0) then finds the tile stores landed instead of holding the MFMAs
         // behind them (mlp512 35.55 -> 35.43 us median, profiles/r03_ab_latepub.json;
-        // the GRU body measured no gain: 60.05 vs 60.16 us, so it keeps the early flag)
+        // in the GRU body it measured 60.09 -> 60.63 us per tick and no change over
+        // 100-tick sequences, profiles/r03_ab_latepub_gru.json: it keeps the early flag)
         [&]<int... I>(std::integer_sequence<int, I...>) {
           ((w4_chunk<TPW, (I & 3), RD, true, true>(accn, f, v[I], ws, vo, ((t0 + I + RD) & (CH - 1)) * CSB),
             I == 0 ? publish() : void()),
