@@ -92,15 +92,19 @@ class InferenceSession:
             raise ValueError(f"missing input '{in_name}'")
         x = np.asarray(input_feed[in_name], dtype=np.float32).reshape(-1, e.in_dim)
         B = x.shape[0]
-        # recurrent state: GRU h [H]; LSTM h [H] | c [H] (the engine keeps both per robot)
-        parts = [n for n, _ in e.inputs[1:]]           # h_in (, c_in)
-        width = e.hidden_dim // max(1, len(parts)) if e.hidden_dim else 0
+        # recurrent state: GRU h [H]; LSTM h [H] | c [H] (the engine keeps both per robot).
+        # The loader lists the state inputs / outputs as (h, c), whatever their order in the
+        # graph (traced to the cell's initial_h / initial_c and Y_h / Y_c by name); the
+        # split follows from the cell, not from how many of them the graph exports.
+        nparts = 2 if e.cost["cell"] == "LSTM" else 1
+        parts = [n for n, _ in e.inputs[1:1 + nparts]]  # h_in (, c_in), possibly none
+        width = e.hidden_dim // nparts if e.hidden_dim else 0
         if e.hidden_dim:
             # explicit recurrent I/O when the caller feeds/asks for it; otherwise engine-resident
             fed = [n in input_feed for n in parts]
             if any(fed):
-                cur = e.get_hidden(B).reshape(B, len(parts), width) if not all(fed) else \
-                    np.empty((B, len(parts), width), np.float32)
+                cur = e.get_hidden(B).reshape(B, nparts, width) if not all(fed) or len(parts) < nparts else \
+                    np.empty((B, nparts, width), np.float32)
                 for k, n in enumerate(parts):
                     if n in input_feed:
                         cur[:, k] = np.asarray(input_feed[n], np.float32).reshape(B, width)
@@ -108,8 +112,8 @@ class InferenceSession:
         y = e.run(x)
         results = {e.outputs[0][0]: y}
         if e.hidden_dim and len(e.outputs) > 1:
-            st = e.get_hidden(B).reshape(B, len(parts), width)
-            for k, (n, _) in enumerate(e.outputs[1:1 + len(parts)]):
+            st = e.get_hidden(B).reshape(B, nparts, width)
+            for k, (n, _) in enumerate(e.outputs[1:1 + nparts]):
                 results[n] = np.ascontiguousarray(st[:, k]).reshape(1, B, width)
         names = output_names or [n for n, _ in e.outputs]
         return [results[n] for n in names]

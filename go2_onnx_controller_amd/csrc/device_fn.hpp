@@ -22,12 +22,20 @@ __device__ __forceinline__ float sigmoid_fast(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
+// ONNX Clip (opset 11+): std::min(std::max(x, lo), hi) as onnxruntime computes it,
+// so a NaN passes through (fminf / fmaxf would return the bound instead).
+__device__ __forceinline__ float clip_nan(float x, float lo, float hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+
 // Activation with the kind known at compile time: epilogues dispatch ONCE per
 // tile group (a runtime switch per element made hipcc emit every activation's
 // code, an IEEE divide and a vmcnt(0) wait for each of the 16 elements per lane:
-// measured 4.4K cycles per layer epilogue).
+// measured 4.4K cycles per layer epilogue). alpha / beta: the node's attributes
+// (Elu / LeakyRelu alpha; Clip min / max; Selu alpha / gamma; HardSigmoid alpha /
+// beta), Act in onnx_model.hpp.
 template <int ACT>
-__device__ __forceinline__ float act_t(float alpha, float x) {
+__device__ __forceinline__ float act_t(float alpha, float beta, float x) {
 #ifdef GO2PI_DIAG_NOEPI
   return x;
 #endif
@@ -36,17 +44,31 @@ __device__ __forceinline__ float act_t(float alpha, float x) {
   else if constexpr (ACT == 3) return tanhf(x);                       // Tanh
   else if constexpr (ACT == 4) return sigmoid_fast(x);                // Sigmoid
   else if constexpr (ACT == 5) return x >= 0.f ? x : alpha * x;       // LeakyRelu
+  else if constexpr (ACT == 6) return clip_nan(x, alpha, beta);       // Clip (ReLU6: 0, 6)
+  else if constexpr (ACT == 7) return x > 0.f ? beta * x : beta * (alpha * expm1_neg(x));  // Selu
+  else if constexpr (ACT == 8) return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));             // Softplus
+  else if constexpr (ACT == 9) return clip_nan(alpha * x + beta, 0.f, 1.f);                // HardSigmoid
+  else if constexpr (ACT == 10) return x * clip_nan(alpha * x + beta, 0.f, 1.f);           // HardSwish
+  else if constexpr (ACT == 11) return x / (1.f + fabsf(x));                               // Softsign
   else return x;
 }
 
-__device__ __forceinline__ float act_fn(int act, float alpha, float x) {
+#define GO2PI_NUM_ACTS 12
+
+__device__ __forceinline__ float act_fn(int act, float alpha, float beta, float x) {
   switch (act) {
-    case 1: return act_t<1>(alpha, x);
-    case 2: return act_t<2>(alpha, x);
-    case 3: return act_t<3>(alpha, x);
-    case 4: return act_t<4>(alpha, x);
-    case 5: return act_t<5>(alpha, x);
-    default: return act_t<0>(alpha, x);
+    case 1: return act_t<1>(alpha, beta, x);
+    case 2: return act_t<2>(alpha, beta, x);
+    case 3: return act_t<3>(alpha, beta, x);
+    case 4: return act_t<4>(alpha, beta, x);
+    case 5: return act_t<5>(alpha, beta, x);
+    case 6: return act_t<6>(alpha, beta, x);
+    case 7: return act_t<7>(alpha, beta, x);
+    case 8: return act_t<8>(alpha, beta, x);
+    case 9: return act_t<9>(alpha, beta, x);
+    case 10: return act_t<10>(alpha, beta, x);
+    case 11: return act_t<11>(alpha, beta, x);
+    default: return act_t<0>(alpha, beta, x);
   }
 }
 
@@ -59,20 +81,29 @@ __device__ __forceinline__ void with_act(int act, F &&f) {
     case 3: f(std::integral_constant<int, 3>{}); break;
     case 4: f(std::integral_constant<int, 4>{}); break;
     case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: f(std::integral_constant<int, 9>{}); break;
+    case 10: f(std::integral_constant<int, 10>{}); break;
+    case 11: f(std::integral_constant<int, 11>{}); break;
     default: f(std::integral_constant<int, 0>{}); break;
   }
 }
 
+// The action epilogue (go2pi_opts and a graph's trailing Clip / scalar Mul):
+// y <- scale * clip(tanh?(y), lo, hi); the clip passes a NaN through, as ONNX Clip.
 __device__ __forceinline__ float post_fn(const DevProgram &P, float v) {
   if (P.post_tanh) v = tanhf(v);
-  v = fminf(fmaxf(v, P.clip_lo), P.clip_hi);
+  v = clip_nan(v, P.clip_lo, P.clip_hi);
   return v * P.scale;
 }
 
 __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
   if (P.pre_sub) v -= P.pre_sub[P.pre_sub_bcast ? 0 : k];
   if (P.pre_div) v /= P.pre_div[P.pre_div_bcast ? 0 : k];
-  if (P.obs_clip > 0.f) v = fminf(fmaxf(v, -P.obs_clip), P.obs_clip);
+  if (P.pre_mul) v *= P.pre_mul[P.pre_mul_bcast ? 0 : k];
+  if (P.pre_clip) v = clip_nan(v, P.obs_lo, P.obs_hi);
   return v;
 }
 

@@ -61,7 +61,9 @@ inline int ceil64(int x) { return (x + 63) & ~63; }
 std::mutex g_pin_mu;
 std::vector<std::pair<size_t, void *>> g_pin_free;  // (bytes, block)
 
-void *pin_take(size_t bytes) {
+// bytes: in, the size wanted; out, the size of the block handed out (a reused block
+// may be larger), which is what pin_give must get back
+void *pin_take(size_t &bytes) {
   bytes = (bytes + 4095) & ~(size_t)4095;
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
@@ -71,6 +73,7 @@ void *pin_take(size_t bytes) {
         best = i;
     if (best < g_pin_free.size()) {
       void *p = g_pin_free[best].second;
+      bytes = g_pin_free[best].first;
       g_pin_free.erase(g_pin_free.begin() + (long)best);
       return p;
     }
@@ -82,7 +85,7 @@ void *pin_take(size_t bytes) {
 
 void pin_give(void *p, size_t bytes) {
   std::lock_guard<std::mutex> lk(g_pin_mu);
-  g_pin_free.emplace_back((bytes + 4095) & ~(size_t)4095, p);
+  g_pin_free.emplace_back(bytes, p);
 }
 
 // Every entry point leaves the calling thread's current HIP device as it found it
@@ -104,7 +107,7 @@ namespace {
 void res_register(go2pi_engine *e);
 unsigned *yield_word(int device);
 void res_unregister(go2pi_engine *e);
-void evict_residents(const go2pi_engine *self);
+void evict_residents(const go2pi_engine *self, int64_t batch);
 }  // namespace
 
 struct go2pi_engine {
@@ -194,8 +197,9 @@ struct go2pi_engine {
   // pinned, host-mapped (fine-grained) memory and its device alias
   template <class T>
   void palloc(T **host, T **dev, size_t bytes) {
-    void *p = pin_take(bytes);
-    pinned.emplace_back(bytes, p);
+    size_t got = bytes;
+    void *p = pin_take(got);
+    pinned.emplace_back(got, p);  // the block's real size goes back to the cache
     std::memset(p, 0, bytes);
     *host = static_cast<T *>(p);
     if (dev) hip_check(hipHostGetDevicePointer((void **)dev, p, 0), "hipHostGetDevicePointer");
@@ -323,7 +327,24 @@ struct go2pi_engine {
             }
             break;
           }
-          if ((d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) == GO2PI_RES_LEAVE) break;
+          if ((d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) == GO2PI_RES_LEAVE) {
+            // the kernel may have answered this request and then left (a LEAVE header
+            // from evict_residents, or a moved yield counter): its action granules are
+            // acknowledged before the LEAVE done word (resident.hip: vmcnt(0), barrier,
+            // then done), so a rescan after seeing LEAVE finds them if it served the
+            // request. Treating a served request as unserved would run it twice: for a
+            // GRU / LSTM policy, advancing the hidden state twice.
+            int k = 0;
+            while (k < nout && (unsigned)(__atomic_load_n(h_actg + k, __ATOMIC_ACQUIRE) >> 32) == e0) ++k;
+            if (k == nout) {
+              d = e0;
+              for (int j = 0; j < nout; ++j) {
+                const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
+                std::memcpy(h_act + j, &bits, 4);
+              }
+            }
+            break;
+          }
           __builtin_ia32_pause();
           if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
         }
@@ -443,9 +464,12 @@ unsigned *yield_word(int device) {
   return words[device];
 }
 
-void evict_residents(const go2pi_engine *self) {
+// batch: the rows of the launch that follows (one 16-row workgroup each); a launch of
+// at most GO2PI_YIELD_MIN_GRID workgroups fits beside the resident kernels and evicts
+// none (the kernels' own yield bump has the same bound, program.hpp).
+void evict_residents(const go2pi_engine *self, int64_t batch) {
   static const bool off = std::getenv("GO2PI_RES_NO_EVICT") != nullptr;
-  if (off) return;
+  if (off || (batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS <= GO2PI_YIELD_MIN_GRID) return;
   std::lock_guard<std::mutex> lk(g_res_mu);
   for (go2pi_engine *o : g_res_engines)
     if (o != self && o->device == self->device && o->res_flag.load() == 1)
@@ -525,7 +549,7 @@ bool w4_eligible(const go2pi_engine &e, const go2pi::Model &m) {
   if (!(tpw == 2 || tpw == 4 || tpw == 8) || t_last > (tpw == 8 ? 1 : 2)) return false;
   for (int l = 0; l + 1 < nl; ++l)
     if (ceil64(m.layers[l].N) != 64 * tpw || m.layers[l].act != m.layers[0].act ||
-        m.layers[l].alpha != m.layers[0].alpha)
+        m.layers[l].alpha != m.layers[0].alpha || m.layers[l].beta != m.layers[0].beta)
       return false;
   return true;
 }
@@ -600,6 +624,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     L.N = m.layers[l].N;
     L.act = m.layers[l].act;
     L.alpha = m.layers[l].alpha;
+    L.beta = m.layers[l].beta;
     maxw = std::max({maxw, kp, np});
     flops += 2.0 * m.layers[l].K * m.layers[l].N;
     wbytes += 4.0 * ((double)m.layers[l].K * m.layers[l].N + m.layers[l].N);
@@ -681,7 +706,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     }
   }
 
-  // prologue: model-defined (Sub/Div nodes) and/or opts-defined normalisation
+  // prologue: model-defined (Sub/Div/Mul/Clip nodes) and/or opts-defined normalisation
   std::vector<float> sub = m.pre_sub, div = m.pre_div;
   if (e.opts.obs_mean) {
     if (!sub.empty()) throw ApiError("model already normalises its input; obs_mean not allowed", GO2PI_E_INVALID);
@@ -693,7 +718,28 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   }
   if (!sub.empty()) { p.pre_sub = e.upload(sub); p.pre_sub_bcast = sub.size() == 1; }
   if (!div.empty()) { p.pre_div = e.upload(div); p.pre_div_bcast = div.size() == 1; }
-  p.obs_clip = e.opts.obs_clip;
+  if (!m.pre_mul.empty()) {
+    if (e.opts.obs_mean || e.opts.obs_std)
+      throw ApiError("model already scales its input; obs_mean / obs_std not allowed", GO2PI_E_INVALID);
+    p.pre_mul = e.upload(m.pre_mul);
+    p.pre_mul_bcast = m.pre_mul.size() == 1;
+  }
+  p.obs_lo = m.pre_lo;
+  p.obs_hi = m.pre_hi;
+  if (e.opts.obs_clip > 0.f) {
+    p.obs_lo = std::max(p.obs_lo, -e.opts.obs_clip);
+    p.obs_hi = std::min(p.obs_hi, e.opts.obs_clip);
+  }
+  p.pre_clip = (std::isfinite(p.obs_lo) || std::isfinite(p.obs_hi)) ? 1 : 0;
+  // action epilogue: the graph's trailing Clip / scalar Mul (post_fn: clip, then
+  // scale), then the options'. The options apply after the graph, which post_fn's
+  // fixed order tanh -> clip -> scale can only express when the graph adds no scale
+  // (and, for tanh, no clip either).
+  const bool m_clip = std::isfinite(m.clip_lo) || std::isfinite(m.clip_hi);
+  if (e.opts.action_tanh && (m_clip || m.post_scale != 1.f))
+    throw ApiError("action_tanh on a graph that clips or scales its output is not supported", GO2PI_E_INVALID);
+  if (e.opts.action_clip > 0.f && m.post_scale != 1.f)
+    throw ApiError("action_clip on a graph that scales its output is not supported", GO2PI_E_INVALID);
   p.post_tanh = e.opts.action_tanh ? 1 : 0;
   p.clip_lo = m.clip_lo;
   p.clip_hi = m.clip_hi;
@@ -701,7 +747,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.clip_lo = std::max(p.clip_lo, -e.opts.action_clip);
     p.clip_hi = std::min(p.clip_hi, e.opts.action_clip);
   }
-  p.scale = (e.opts.action_scale != 0.f) ? e.opts.action_scale : 1.f;
+  p.scale = m.post_scale * ((e.opts.action_scale != 0.f) ? e.opts.action_scale : 1.f);
 
   const size_t lds = go2pi::fused_lds_bytes(p, e.waves);
   if (lds > 160 * 1024)
@@ -794,14 +840,16 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.in_dim_hot = p.in_dim;
     p.hid_act = p.L[0].act;
     p.hid_alpha = p.L[0].alpha;
+    p.hid_beta = p.L[0].beta;
     p.head_act = H.act;
     p.head_alpha = H.alpha;
+    p.head_beta = H.beta;
     p.post_plain = (!p.post_tanh && std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) &&
                     p.clip_hi > 0 && p.scale == 1.f) ? 1 : 0;
     p.w4_c0m = p.c0 % 4;
     // the lean kernel: no prologue / epilogue arithmetic, no recurrent cell, and an
     // LDS row no wider than the hidden layers
-    p.w4_plain = !p.has_gru && !p.pre_sub && !p.pre_div && !(p.obs_clip > 0.f) && !p.post_tanh &&
+    p.w4_plain = !p.has_gru && !p.pre_sub && !p.pre_div && !p.pre_mul && !p.pre_clip && !p.post_tanh &&
                  std::isinf(p.clip_lo) && p.clip_lo < 0 && std::isinf(p.clip_hi) && p.clip_hi > 0 &&
                  p.scale == 1.f && p.lds_stride == 64 * p.w4_tpw + 4 && !std::getenv("GO2PI_NO_PLAIN");
     // the lean kernel's compile-time activation: Elu (the exported rsl_rl / Isaac policies'), else runtime
@@ -824,7 +872,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.cost.weight_bytes = wbytes;
   e.cost.io_bytes_per_row = 4.0 * (m.in_dim + m.out_dim) + (m.has_gru ? 8.0 * p.gru.sw : 0.0);
   e.cost.n_layers = p.nl;
-  e.cost.has_gru = p.has_gru;
+  e.cost.has_gru = p.has_gru ? (p.gru.cell == 1 ? 2 : 1) : 0;  // 1 GRU, 2 LSTM (go2pi.h)
 }
 
 // Every C-ABI entry point runs through here: exceptions become status codes, and
@@ -975,7 +1023,7 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
       return GO2PI_OK;
     }
     e->resident_stop();
-    if (batch > GO2PI_SMALL_MAXB || !e->latency_ok) evict_residents(e);  // a batched (fused) launch follows
+    if (batch > GO2PI_SMALL_MAXB || !e->latency_ok) evict_residents(e, batch);  // a batched (fused) launch follows
     const size_t in_b = sizeof(float) * (size_t)batch * e->model.in_dim;
     const size_t out_b = sizeof(float) * (size_t)batch * e->model.out_dim;
     if (batch <= GO2PI_SMALL_MAXB) {
@@ -1014,7 +1062,7 @@ int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int6
     if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     e->check_handoff();  // a failure of an earlier asynchronous launch surfaces here (or at go2pi_sync)
-    if (!e->use_latency(batch)) evict_residents(e);
+    if (!e->use_latency(batch)) evict_residents(e, batch);
     e->enqueue(obs_dev, act_dev, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
   });
@@ -1032,7 +1080,7 @@ int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_
       throw ApiError("sequence too large", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    evict_residents(e);
+    evict_residents(e, batch);
     hip_check(go2pi::launch_policy_fused(e->prog, e->d_prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch,
                                          (int)steps, s),
               "fused sequence launch");
@@ -1237,7 +1285,7 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
       e->resident_stop();
     }
     const bool single = !served && small && e->use_latency(batch) && e->done_ok;
-    if (!single && !served) evict_residents(e);  // a batched (fused) launch follows
+    if (!single && !served) evict_residents(e, batch);  // a batched (fused) launch follows
     if (!served) e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
     if (small) {
       const bool synced = served || (single && e->spin_done());
@@ -1276,7 +1324,7 @@ int go2pi_controller_step_device(go2pi_engine *e, const float *state, const floa
     // a live resident kernel shares the granules, epoch and error words the batch <= 8
     // launch uses: it leaves first (as for every other call on the engine)
     e->resident_stop();
-    if (!(e->use_latency(batch) && e->done_ok)) evict_residents(e);
+    if (!(e->use_latency(batch) && e->done_ok)) evict_residents(e, batch);
     go2pi::DevCtl c{e->d_ctl, state, joy, obs, action, q_des, kp, kd, status};
     e->enqueue_ctl(c, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
@@ -1358,7 +1406,8 @@ int go2pi_inspect_model(const char *path, char *buf, size_t cap) {
     for (size_t l = 0; l < m.layers.size(); ++l) {
       const auto &d = m.layers[l];
       j += (l ? "," : "") + std::string("{\"K\":") + std::to_string(d.K) + ",\"N\":" + std::to_string(d.N) +
-           ",\"act\":" + std::to_string(d.act) + ",\"alpha\":" + num(d.alpha) + ",\"w_sum\":" + num(sum(d.W)) +
+           ",\"act\":" + std::to_string(d.act) + ",\"alpha\":" + num(d.alpha) + ",\"beta\":" + num(d.beta) +
+           ",\"w_sum\":" + num(sum(d.W)) +
            ",\"b_sum\":" + num(sum(d.b)) + "}";
     }
     j += "],\"gru\":";
@@ -1370,7 +1419,9 @@ int go2pi_inspect_model(const char *path, char *buf, size_t cap) {
     else
       j += "null";
     j += ",\"pre_sub\":" + std::to_string(m.pre_sub.size()) + ",\"pre_div\":" + std::to_string(m.pre_div.size()) +
-         ",\"clip\":[" + num(m.clip_lo) + "," + num(m.clip_hi) + "]}";
+         ",\"pre_mul\":" + std::to_string(m.pre_mul.size()) + ",\"pre_clip\":[" + num(m.pre_lo) + "," +
+         num(m.pre_hi) + "],\"clip\":[" + num(m.clip_lo) + "," + num(m.clip_hi) + "],\"post_scale\":" +
+         num(m.post_scale) + "}";
     const size_t k = std::min(cap - 1, j.size());
     std::memcpy(buf, j.data(), k);
     buf[k] = 0;

@@ -16,36 +16,43 @@ namespace go2pi {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#if defined(GO2PI_DIAG_RD2)
-#define GO2PI_RING_RD 2
-#elif defined(GO2PI_DIAG_RD3)
-#define GO2PI_RING_RD 3
-#else
-#define GO2PI_RING_RD 1  // chunks ahead of the weight-fragment ring at 4 waves per workgroup (2, 3: slower)
-#endif
+// chunks ahead of the weight-fragment ring of the generic body at 4 waves per
+// workgroup (2 and 3 measured slower: 40.2 / 42.2 vs 39.5 us)
+#define GO2PI_RING_RD 1
 // the 4-wave pipeline's ring depth by tiles per wave: a chunk is 4 * TPW MFMAs
 // (32 cycles each), and a fragment must be issued >= ~1K cycles (an L2 round trip
 // under load) before its MFMA
-#ifndef GO2PI_DIAG_RD2
-#ifndef GO2PI_DIAG_RD3
 #define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? 1 : ((TPW) >= 4 ? 2 : 3))
-#endif
-#endif
-#ifndef GO2PI_W4_RD
-#define GO2PI_W4_RD(TPW) GO2PI_RING_RD
-#endif
-#ifndef GO2PI_WPOL  // weight-fragment load policy: 0 plain, 1 nt, 2 sc1 (L1 bypass)
-#if defined(GO2PI_DIAG_NT)
-#define GO2PI_WPOL 1
-#elif defined(GO2PI_DIAG_SC1)
-#define GO2PI_WPOL 2
-#else
-#define GO2PI_WPOL 0
-#endif
-#endif
 #define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
 
-// Diagnostic ablation builds only (tools/diag.sh; outputs are wrong by design):
+// Clock stamps (GO2PI_DIAG_CLOCK builds, tools/clock_probe.py): s_memtime (or the
+// 100 MHz s_memrealtime) of a workgroup's phases into P.stamps[block][slot]. In the
+// shipped build the macros are empty: no load, no store, no condition evaluated.
+#ifdef GO2PI_DIAG_CLOCK
+#define GO2PI_STAMP_AT(row, cond, slot)                                  \
+  do {                                                                   \
+    if ((row) && (cond)) (row)[slot] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#define GO2PI_STAMP(P, cond, slot) \
+  GO2PI_STAMP_AT((P).stamps ? (P).stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, cond, slot)
+#define GO2PI_STAMP_RT(P, cond, slot)                                                                       \
+  do {                                                                                                      \
+    if ((P).stamps && (cond)) (P).stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define GO2PI_STAMP_AT(row, cond, slot) \
+  do {                                  \
+    (void)sizeof(row);                  \
+  } while (0)
+#define GO2PI_STAMP(P, cond, slot) \
+  do {                             \
+  } while (0)
+#define GO2PI_STAMP_RT(P, cond, slot) \
+  do {                                \
+  } while (0)
+#endif
+
+// Diagnostic ablation builds only (tools/bound_probe.sh; outputs are wrong by design):
 //   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
 //   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -74,9 +81,6 @@ __device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int 
   (void)p;
   (void)cs;
   return make_float4(v, v, v, v);
-#elif GO2PI_WPOL == 1
-  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p + c * cs));
-  return make_float4(v.x, v.y, v.z, v.w);
 #else
   return p[c * cs];
 #endif
@@ -84,8 +88,7 @@ __device__ __forceinline__ float4 load_frag(const float4 *p, int c, int cs, int 
 
 // Weight-fragment stream over a buffer resource: one SGPR descriptor per layer,
 // a per-lane byte offset per tile and the chunk offset folded into the scalar
-// offset. GO2PI_WPOL == 2 sets sc1 on the loads (served by the XCD's L2,
-// bypassing the CU's 32 KiB L1, which the fragments in flight would overrun).
+// offset (sc1 or nt on these loads measured no change).
 struct WStream {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ explicit WStream(const void *base)
@@ -95,8 +98,7 @@ struct WStream {
     const float v = __int_as_float(0x3c000000 ^ ((voff + soff) & 0xff));
     return make_float4(v, v, v, v);
 #else
-    constexpr int AUX = GO2PI_WPOL == 2 ? 16 : (GO2PI_WPOL == 1 ? 2 : 0);
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 #endif
   }
 };
@@ -111,73 +113,12 @@ struct WStream {
 // order (hipcc otherwise sinks loads next to their uses). Tiles beyond T clamp
 // to T - 1 (duplicate loads, results unused); loads past c1 clamp to c1 - 1.
 // Requires (c1 - c0) % 4 == 0 (K padded to 64).
-//
-// Hand-off between two wide layers without a workgroup barrier (Handoff):
-// wave w publishes flags[w] = ep once its tiles of a layer are stored in LDS;
-// a wave of the next layer starts on the 4-chunk group that its own tiles form
-// (rotated chunk order, g0) and, before reading any group's A operands, waits
-// until that group's producer waves have published ep. A wave therefore reads
-// a group only after its producers stored it (RAW), and every producer sets
-// its flag only after its own contraction of the layer before, which read the
-// buffer this layer's epilogue overwrites (ping-pong WAR): by the end of its
-// contraction a consumer has seen every producer's flag. The rotation changes
-// the summation order of K chunks per wave, identically for every robot row.
-struct Handoff {
-  const int *flags;  // LDS, one int per wave; nullptr: the input is complete (barrier before)
-  int ep;            // epoch every producer of the input must have published
-  int tpw;           // producer tiles per wave
-  // cross-layer prefetch (barrier hand-off only): this wave's first tile
-  // group's chunk-0 fragments, loaded before the barrier (prefetch_first)
-  float4 pre[4];
-  int npre;       // valid entries of pre (0: none)
-  unsigned *err;  // set to 1 when a poll runs out of its bound (the engine raises it)
-};
-
-// Issue this wave's first weight fragments of layer L (chunk 0 of its first
-// tile group) before the barrier that completes L's input: they do not depend
-// on the activations, and the barrier waits on LDS only (lgkmcnt), so the
-// loads stay in flight across it. Same addresses as dense_acc's first loads.
-template <int NW>
-__device__ __forceinline__ void prefetch_first(const DevLayer &L, int wave, int lane, Handoff &h) {
-  const int T = L.N_pad >> 4;
-  if (T < NW) return;  // narrow layer: split-K path, no tile groups
-  constexpr int NP = NW >= 16 ? 2 : 4;  // min(G, 4)
-  const int t = wave * ((T + NW - 1) / NW);
-  const float4 *W = reinterpret_cast<const float4 *>(L.w);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) h.pre[i] = load_frag(W + (size_t)min(t + i, T - 1) * 64 + lane, 0, 0, i);
-  h.npre = NP;
-}
-
-__device__ __forceinline__ void handoff_wait(const Handoff &h, int c, int nw, int lane, bool &all) {
-  if (!h.flags || all) return;
-  const int wlo = c / h.tpw, whi = (c + 3) / h.tpw;  // producers of chunks c..c+3 (= tiles)
-  const unsigned long long need = ((2ull << whi) - 1) & ~((1ull << wlo) - 1);
-  for (int it = 0; it < (1 << 20); ++it) {  // bounded: ~30 ms, a protocol bug must not hang the GPU
-    const int f =
-        lane < nw ? __hip_atomic_load(h.flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : h.ep;
-    const unsigned long long ok = __ballot(f >= h.ep);
-    if (ok == ~0ull) {
-      all = true;  // every producer is done: no further polls this layer
-      break;
-    }
-    if ((ok & need) == need) break;
-    if (it == (1 << 20) - 1 && lane == 0 && h.err)  // never silently: outputs of this launch are invalid
-      __hip_atomic_store(h.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");  // the group's A-operand reads stay after the poll
-}
-
-__device__ __forceinline__ void handoff_publish(int *flags, int wave, int lane, int ep) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
-  if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
+// (A flag hand-off between two wide layers instead of the workgroup barrier, and
+// fragments prefetched across that barrier, both measured slower in this body:
+// mlp512 47.8 vs 45.6 us, gru256 78.4 vs 76.4 us)
 template <int TPW>
 __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *__restrict__ W, int TL, int t_first,
-                                          int T, int c0, int c1, int lane, f32x4 (&acc)[TPW],
-                                          const Handoff &h = Handoff{nullptr, 0, 1}, int g0 = 0, int nw = 0) {
+                                          int T, int c0, int c1, int lane, f32x4 (&acc)[TPW]) {
   const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
   const WStream ws(W);
   int vo[TPW];                // per-lane byte offset of each tile's fragment in chunk 0
@@ -185,45 +126,24 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
 #pragma unroll
   for (int i = 0; i < TPW; ++i) vo[i] = (min(t_first + i, T - 1) * 64 + lane) * 16;
   if (c0 >= c1) return;
-  const int NG = (c1 - c0) >> 2;
-  int g = g0 % NG;
   float4 cur[TPW];
-  if (TPW <= 4 && !h.flags && h.npre >= TPW && c0 == 0) {
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) cur[i] = h.pre[i < 4 ? i : 0];  // prefetched before the barrier
-  } else {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) cur[i] = ws.ld(vo[i], (c0 + 4 * g) * csb);
-  }
+  for (int i = 0; i < TPW; ++i) cur[i] = ws.ld(vo[i], c0 * csb);
   // the last 4-chunk group is peeled (TAIL) so no prefetch is issued past the end:
   // a trailing load would only be waited for by the epilogue
   // (A operands are read per 4-chunk group; double-buffering them across groups
   // measured slower: 100.4K vs 97.8K cycles per workgroup; fragments 2 chunks
   // ahead instead of 1 measured slower too: 98.1K vs 96.2K)
-  auto group = [&](int c, int cnext, auto tail_k) {
+  auto group = [&](int c, auto tail_k) {
     constexpr bool TAIL = decltype(tail_k)::value;
     float4 a[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4 *>(xrow + (c + u) * 16);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int cn = u < 3 ? c + u + 1 : cnext;  // the next group's first chunk (rotated order)
+      const int cn = c + u + 1;
       const bool LOAD = !(TAIL && u == 3);  // folded after unrolling
       float4 nxt[TPW];
-#ifdef GO2PI_DIAG_TILEOUTER  // previous order: each tile's 4 k-steps back to back
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        acc[i] = mfma4(cur[i].x, a[u].x, acc[i]);
-        acc[i] = mfma4(cur[i].y, a[u].y, acc[i]);
-        acc[i] = mfma4(cur[i].z, a[u].z, acc[i]);
-        acc[i] = mfma4(cur[i].w, a[u].w, acc[i]);
-        if (LOAD) {
-          __builtin_amdgcn_sched_barrier(0);
-          nxt[i] = ws.ld(vo[i], cn * csb);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-#else
       // k-step outer, tile inner: consecutive MFMAs hit different accumulators,
       // so one wave issues at the 32-cycle rate instead of waiting out the
       // 40-cycle dependent-accumulator latency. Each accumulator still sees its
@@ -242,22 +162,15 @@ __device__ __forceinline__ void dense_acc(const float *X, int xs, const float4 *
           }
         }
       }
-#endif
       if (LOAD) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) cur[i] = nxt[i];
       }
     }
   };
-  bool all = false;
-  for (int k = 0; k + 1 < NG; ++k) {
-    const int gn = g + 1 == NG ? 0 : g + 1;
-    handoff_wait(h, c0 + 4 * g, nw, lane, all);
-    group(c0 + 4 * g, c0 + 4 * gn, std::false_type{});
-    g = gn;
-  }
-  handoff_wait(h, c0 + 4 * g, nw, lane, all);
-  group(c0 + 4 * g, 0, std::true_type{});
+  int c = c0;
+  for (; c + 4 < c1; c += 4) group(c, std::false_type{});
+  group(c, std::true_type{});
 }
 
 // Contraction for one wave per SIMD (4 waves per workgroup): a wave owns TPW
@@ -346,16 +259,16 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
   const int rob = lane & 15, n0 = (lane >> 4) << 2;
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
-    const float alpha = L.alpha;
+    const float alpha = L.alpha, beta = L.beta;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int t = t_first + i;
       if (t >= T) continue;
       float4 v;
-      v.x = act_t<ACT>(alpha, acc[i][0] + bv[i].x);
-      v.y = act_t<ACT>(alpha, acc[i][1] + bv[i].y);
-      v.z = act_t<ACT>(alpha, acc[i][2] + bv[i].z);
-      v.w = act_t<ACT>(alpha, acc[i][3] + bv[i].w);
+      v.x = act_t<ACT>(alpha, beta, acc[i][0] + bv[i].x);
+      v.y = act_t<ACT>(alpha, beta, acc[i][1] + bv[i].y);
+      v.z = act_t<ACT>(alpha, beta, acc[i][2] + bv[i].z);
+      v.w = act_t<ACT>(alpha, beta, acc[i][3] + bv[i].w);
       if (!last) {
         *reinterpret_cast<float4 *>(Y + rob * ys + t * 16 + n0) = v;
         if constexpr (KEEP) keep[i] = v;
@@ -384,7 +297,7 @@ template <int TPW, int HT, int RD = 0>
 __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int t_first, int T, int C, int lane, bool last, float *out,
                                             const CtlView ctl, int row0, int B, const DevLayer *HL,
-                                            f32x4 (&hacc)[HT > 0 ? HT : 1], const Handoff &h, int g0, int nw) {
+                                            f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   constexpr int HN = HT > 0 ? HT : 1;
   f32x4 acc[TPW];
   float4 bv[TPW];
@@ -400,25 +313,18 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
   }
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef GO2PI_DIAG_CLOCK  // per-wave phase stamps inside layer 1: entry, contraction done, epilogue done
-  unsigned long long *st = (P.stamps && &L == &P.L[1] && lane == 0)
-                               ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * (threadIdx.x >> 6)
-                               : nullptr;
-  if (st) st[0] = __builtin_amdgcn_s_memtime();
-#endif
+  // per-wave phase stamps inside layer 1: entry, contraction done, epilogue done
+  [[maybe_unused]] const bool st = &L == &P.L[1] && lane == 0;
+  [[maybe_unused]] const int sts = 16 + 3 * (threadIdx.x >> 6);
+  GO2PI_STAMP(P, st, sts);
   if constexpr (RD > 0)
     dense_acc_ring<TPW, RD>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, C, lane, acc);
   else
-    dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc, h, g0,
-                   nw);
-#ifdef GO2PI_DIAG_CLOCK
-  if (st) st[1] = __builtin_amdgcn_s_memtime();
-#endif
+    dense_acc<TPW>(X, xs, reinterpret_cast<const float4 *>(L.w), L.N_pad >> 4, t_first, T, 0, C, lane, acc);
+  GO2PI_STAMP(P, st, sts + 1);
   float4 yv[TPW];
   dense_store<TPW, (HT > 0)>(P, L, acc, bv, t_first, T, lane, last, Y, xs, out, ctl, row0, B, yv);
-#ifdef GO2PI_DIAG_CLOCK
-  if (st) st[2] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP(P, st, sts + 2);
   if constexpr (HT > 0) {
     // the head's B operand for k-chunk t_first + i is exactly the float4 this
     // lane just stored (its robot, k = 16t + 4(lane >> 4) + j): use the registers
@@ -441,8 +347,7 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
                                             int t_first, int T, int C, int lane, bool last, float *out,
                                             const CtlView ctl, int row0, int B) {
   f32x4 none[1];
-  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none,
-                      Handoff{nullptr, 0, 1}, 0, 0);
+  dense_group<TPW, 0>(P, L, X, Y, xs, t_first, T, C, lane, last, out, ctl, row0, B, nullptr, none);
 }
 
 // Tiles of a wide layer split over the NW waves (full K per wave), optionally
@@ -450,37 +355,29 @@ __device__ __forceinline__ void dense_group(const DevProgram &P, const DevLayer 
 template <int NW, int HT>
 __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             int wave, int lane, bool last, float *out, const CtlView ctl, int row0,
-                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1],
-                                            const Handoff &h) {
+                                            int B, const DevLayer *HL, f32x4 (&hacc)[HT > 0 ? HT : 1]) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   // largest tile group per pass: bounded so the accumulators fit the VGPR
   // budget of NW waves per CU (512 / (NW/4) registers per lane)
-#ifdef GO2PI_DIAG_G2
-  constexpr int G = 2;  // variant: smaller tile groups (epilogue of one group beside MFMAs of the next)
-#else
+  // (2-tile groups at 8 waves measured slower: 50.5 vs 44.5 us)
   constexpr int G = NW >= 16 ? 2 : (NW >= 8 ? 4 : 8);
-#endif
   // one wave per SIMD: the register-ring contraction (dense_acc_ring)
   constexpr int RD = NW == 4 ? GO2PI_RING_RD : 0;
   const int tpw = (T + NW - 1) / NW;
   int t = wave * tpw;
   const int t_end = min(t + tpw, T);
-  const int g0 = h.flags ? (wave * h.tpw) >> 2 : 0;  // the chunk group this wave produced itself
-  Handoff hh = h;  // prefetched fragments (hh.npre) belong to the first group only
   for (; t + G <= t_end; t += G) {
-    dense_group<G, HT, RD>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
-    hh.npre = 0;
+    dense_group<G, HT, RD>(P, L, X, Y, xs, t, T, C, lane, last, out, ctl, row0, B, HL, hacc);
   }
   const int rem = t_end - t;
   if (G > 4 && rem > 4)
-    dense_group<G, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<G, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
   else if (G > 2 && rem > 2)
-    dense_group<(G > 4 ? 4 : G), HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0,
-                                     NW);
+    dense_group<(G > 4 ? 4 : G), HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
   else if (rem == 2)
-    dense_group<2, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<2, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
   else if (rem == 1)
-    dense_group<1, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc, hh, g0, NW);
+    dense_group<1, HT, RD>(P, L, X, Y, xs, t, t_end, C, lane, last, out, ctl, row0, B, HL, hacc);
 }
 
 // Layer with the final layer fused in (P.head_fuse = HT tiles): per-wave head
@@ -488,11 +385,11 @@ __device__ __forceinline__ void dense_tiles(const DevProgram &P, const DevLayer 
 template <int NW, int HT>
 __device__ __forceinline__ void dense_layer_head(const DevProgram &P, const DevLayer &L, const DevLayer &HL,
                                                  const float *X, float *Y, int xs, f32x4 *scratch, int wave,
-                                                 int lane, int row0, int B, const Handoff &hin) {
+                                                 int lane, int row0, int B) {
   f32x4 hacc[HT];
 #pragma unroll
   for (int h = 0; h < HT; ++h) hacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc, hin);
+  dense_tiles<NW, HT>(P, L, X, Y, xs, wave, lane, false, nullptr, CtlView{}, row0, B, &HL, hacc);
 #pragma unroll
   for (int h = 0; h < HT; ++h) scratch[(h * NW + wave) * 64 + lane] = hacc[h];
 }
@@ -515,11 +412,11 @@ __device__ __forceinline__ void head_finish(const DevProgram &P, const DevLayer 
 template <int NW>
 __device__ __forceinline__ void dense_layer(const DevProgram &P, const DevLayer &L, const float *X, float *Y, int xs,
                                             f32x4 *scratch, int wave, int lane, bool last, float *out,
-                                            const CtlView ctl, int row0, int B, const Handoff &hin) {
+                                            const CtlView ctl, int row0, int B) {
   const int T = L.N_pad >> 4, C = L.K_pad >> 4;
   if (T >= NW) {
     f32x4 none[1];
-    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none, hin);
+    dense_tiles<NW, 0>(P, L, X, Y, xs, wave, lane, last, out, ctl, row0, B, nullptr, none);
   } else {
     // narrow layer (e.g. the 12-action head): split K over waves, reduce in LDS
     const int ks = NW / T;
@@ -581,7 +478,6 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
   }
   auto step = [&](int c, const float4 &a, f32x4 (&third)[GT], int cn) {
     float4 nz[GT], nr[GT], nh3[GT];
-#ifndef GO2PI_DIAG_TILEOUTER
     // k-step outer over the 3*GT independent gate accumulators (no back-to-back
     // dependent MFMA; per-accumulator k order unchanged), one gate-fragment load
     // after every 4th MFMA
@@ -607,32 +503,6 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
         }
       }
     }
-#else
-#pragma unroll
-    for (int i = 0; i < GT; ++i) {
-      z[i] = mfma4(a.x, cz[i].x, z[i]);
-      z[i] = mfma4(a.y, cz[i].y, z[i]);
-      z[i] = mfma4(a.z, cz[i].z, z[i]);
-      z[i] = mfma4(a.w, cz[i].w, z[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nz[i] = ws.ld(vo[i], cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-      r[i] = mfma4(a.x, cr[i].x, r[i]);
-      r[i] = mfma4(a.y, cr[i].y, r[i]);
-      r[i] = mfma4(a.z, cr[i].z, r[i]);
-      r[i] = mfma4(a.w, cr[i].w, r[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nr[i] = ws.ld(vo[i] + 1024, cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-      third[i] = mfma4(a.x, chh[i].x, third[i]);
-      third[i] = mfma4(a.y, chh[i].y, third[i]);
-      third[i] = mfma4(a.z, chh[i].z, third[i]);
-      third[i] = mfma4(a.w, chh[i].w, third[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      nh3[i] = ws.ld(vo[i] + 2048, cn * csb);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < GT; ++i) {
       cz[i] = nz[i];
@@ -791,13 +661,7 @@ __device__ __forceinline__ void lstm_cell(const DevGru &G, const float *X, const
 // Load spacing: one fragment load after every LSP-th MFMA, so the chunk's TPW
 // loads are issued over its first LSP * TPW MFMAs (the earlier they go out, the
 // longer the last tile's fragment has before its MFMA in the next chunk).
-#if defined(GO2PI_DIAG_LSP1)
-#define GO2PI_W4_LSP 1
-#elif defined(GO2PI_DIAG_LSP4)
-#define GO2PI_W4_LSP 4
-#elif !defined(GO2PI_W4_LSP)
 #define GO2PI_W4_LSP 2
-#endif
 template <int TPW, int S, int RD, bool LOAD, bool PIN>
 __device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b, const WStream &ws,
                                          const int (&vo)[TPW], int soff) {
@@ -819,12 +683,12 @@ __device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW],
 
 // bias + activation of one 16 x 16 tile (output-major: one float4 per lane)
 template <int ACT>
-__device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const float4 &bv) {
+__device__ __forceinline__ float4 w4_epi(float alpha, float beta, const f32x4 &acc, const float4 &bv) {
   float4 v;
-  v.x = act_t<ACT>(alpha, acc[0] + bv.x);
-  v.y = act_t<ACT>(alpha, acc[1] + bv.y);
-  v.z = act_t<ACT>(alpha, acc[2] + bv.z);
-  v.w = act_t<ACT>(alpha, acc[3] + bv.w);
+  v.x = act_t<ACT>(alpha, beta, acc[0] + bv.x);
+  v.y = act_t<ACT>(alpha, beta, acc[1] + bv.y);
+  v.z = act_t<ACT>(alpha, beta, acc[2] + bv.z);
+  v.w = act_t<ACT>(alpha, beta, acc[3] + bv.w);
   return v;
 }
 
@@ -833,13 +697,8 @@ __device__ __forceinline__ float4 w4_epi(float alpha, const f32x4 &acc, const fl
 // tile took it as its C operand), and the x * log2(e) and e - 1 steps run as
 // packed pairs. Per element the same operations as act_t<1> with alpha = 1
 // (x > 0 ? x : exp2(x * log2 e) - 1), so the same bits for the same x.
-//
-// GO2PI_DIAG_ELUMAX (diagnostics, not shipped): the select folded away — e =
-// exp2(x * log2 e) clamped to [0, 1] (the v_exp_f32 clamp bit) is exp(min(x, 0)),
-// and Elu(x) = max(x, e - 1). 35.51 -> 35.37 us at mlp512 (profiles/
-// r03_ab_elumax.json), but the clamp maps a NaN to 0 (DX10 clamp mode), so
-// Elu(NaN) becomes -1 where ONNX Elu propagates the NaN; and in IEEE mode each
-// fmaxf also quiets its register operand (a second v_max per element).
+// (A select-free form, max(x, clamp(e, 0, 1) - 1), measured 0.4 % faster but maps
+// a NaN to -1 where ONNX Elu propagates it: rejected)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool BIN>
 __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv) {
@@ -854,16 +713,6 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
   asm volatile("" : "+v"(x01), "+v"(x23));
   const f32x2 L = {1.4426950408889634f, 1.4426950408889634f};
   const f32x2 t01 = x01 * L, t23 = x23 * L;
-#ifdef GO2PI_DIAG_ELUMAX
-  // (fmed3(v, 0, 1) folds into the exp's clamp bit)
-  f32x2 e01 = {__builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t01.x), 0.f, 1.f),
-               __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t01.y), 0.f, 1.f)};
-  f32x2 e23 = {__builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t23.x), 0.f, 1.f),
-               __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(t23.y), 0.f, 1.f)};
-  e01 -= 1.f;
-  e23 -= 1.f;
-  return make_float4(fmaxf(x01.x, e01.x), fmaxf(x01.y, e01.y), fmaxf(x23.x, e23.x), fmaxf(x23.y, e23.y));
-#else
   f32x2 e01 = {__builtin_amdgcn_exp2f(t01.x), __builtin_amdgcn_exp2f(t01.y)};
   f32x2 e23 = {__builtin_amdgcn_exp2f(t23.x), __builtin_amdgcn_exp2f(t23.y)};
   e01 -= 1.f;
@@ -874,86 +723,6 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
   v.z = x23.x > 0.f ? x23.x : e23.x;
   v.w = x23.y > 0.f ? x23.y : e23.y;
   return v;
-#endif
-}
-
-// One own-phase chunk: the MFMAs of chunk I (B operand b = the epilogue value of
-// the previous layer's tile t0 + I, from registers) with the epilogue of tile
-// I + 1 (accumulator pa, bias pb) woven between them when NEXT. The epilogue is
-// cut into short dependent stages, one after each MFMA from the 4th on (per
-// element: bias add; for Elu also x*log2(e), exp2, alpha*(e-1), select), each
-// pinned by sched_barrier, so its VALU issues in the MFMA pipe's shadow and every
-// dependent stage sits >= 4 MFMAs after its producer. Other activations compute
-// the whole epilogue behind the chunk's MFMAs. Results are bitwise those of
-// w4_epi (the same operations in the same order per element).
-template <int TPW, int S, int RD, int ACT, bool NEXT>
-__device__ __forceinline__ void w4_own_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b,
-                                             const WStream &ws, const int (&vo)[TPW], int soff, const f32x4 &pa,
-                                             const float4 &pb, float alpha, float4 &vn) {
-  constexpr int NM = 4 * TPW;                // MFMAs in the chunk
-  constexpr int NSTG = ACT == 1 ? 5 : 1;    // stages per element
-  constexpr int NS = 4 * NSTG;              // stage slots (4 elements)
-  constexpr int FIRST = NM >= 8 ? 3 : 0;    // first MFMA followed by a stage
-  constexpr int SLOTS = NM - FIRST;
-  constexpr int PER = (NS + SLOTS - 1) / SLOTS;  // stages after each MFMA
-  float t[4], u[4];
-  auto stage = [&](auto q_k) {
-    constexpr int Q = decltype(q_k)::value;  // stage index: element Q % 4, step Q / 4
-    constexpr int E = Q & 3, ST = Q >> 2;
-    // (the empty asm on each stage's result keeps the stages where they are put:
-    // otherwise the SLP vectorizer merges the four elements' stages into packed
-    // ops at the first position)
-    if constexpr (ACT == 1) {
-      if constexpr (ST == 0) {
-        t[E] = pa[E] + f4c(pb, E);
-        asm volatile("" : "+v"(t[E]));
-      } else if constexpr (ST == 1) {
-        u[E] = t[E] * 1.4426950408889634f;
-        asm volatile("" : "+v"(u[E]));
-      } else if constexpr (ST == 2) {
-        u[E] = __builtin_amdgcn_exp2f(u[E]);
-        asm volatile("" : "+v"(u[E]));
-      } else if constexpr (ST == 3) {
-        u[E] = alpha * (u[E] - 1.f);
-        asm volatile("" : "+v"(u[E]));
-      } else {
-        float r = t[E] > 0.f ? t[E] : u[E];
-        asm volatile("" : "+v"(r));
-        if constexpr (E == 0) vn.x = r;
-        else if constexpr (E == 1) vn.y = r;
-        else if constexpr (E == 2) vn.z = r;
-        else vn.w = r;
-      }
-    } else {
-      const float r = act_t<ACT>(alpha, pa[E] + f4c(pb, E));
-      if constexpr (E == 0) vn.x = r;
-      else if constexpr (E == 1) vn.y = r;
-      else if constexpr (E == 2) vn.z = r;
-      else vn.w = r;
-    }
-  };
-  auto stages_after = [&](auto m_k) {
-    constexpr int M = decltype(m_k)::value;
-    if constexpr (NEXT && M >= FIRST) {
-      constexpr int Q0 = (M - FIRST) * PER;
-      [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((Q0 + P < NS ? stage(std::integral_constant<int, (Q0 + P < NS ? Q0 + P : 0)>{}) : void()), ...);
-      }(std::make_integer_sequence<int, PER>{});
-    }
-  };
-  [&]<int... M>(std::integer_sequence<int, M...>) {
-    (([&] {
-       constexpr int J = M / TPW, I = M % TPW;
-       acc[I] = mfma4(f4c(f[S][I], J), f4c(b, J), acc[I]);
-       // the next chunk's fragments as in w4_chunk: one load every LSP MFMAs from the
-       // chunk's start (every 4 left the last ones only 8 MFMAs ahead of their use)
-       constexpr int LSP = GO2PI_W4_LSP;
-       if constexpr (M % LSP == LSP - 1 && M / LSP < TPW) f[(S + RD) & 3][M / LSP] = ws.ld(vo[M / LSP], soff);
-       stages_after(std::integral_constant<int, M>{});
-       __builtin_amdgcn_sched_barrier(0);
-     }()),
-     ...);
-  }(std::make_integer_sequence<int, NM>{});
 }
 
 // Chunks k in [k0, C) of a layer from the LDS activation rows X, chunk
@@ -1041,9 +810,7 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
 template <int GT>
 __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
                                        int lane, float4 (&hn)[GT], unsigned long long *st = nullptr) {
-#ifdef GO2PI_DIAG_CLOCK  // GRU stage marks (wave 0): 43 entry, 44 contraction done, 45 epilogue done
-  if (st && wave == 0 && lane == 0) st[43] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP_AT(st, wave == 0 && lane == 0, 43);  // GRU stage marks (wave 0): 43 entry, 44 contraction, 45 epilogue
   constexpr int NF = 3 * GT;  // gate fragments per chunk
   constexpr int NM = 4 * NF;  // MFMAs per chunk
   const int Cx = G.I_pad >> 4, Ch = G.H >> 4;
@@ -1153,9 +920,7 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
   };
   if ((Cxe & 3) == 3) run(std::integral_constant<int, 1>{});
   else run(std::integral_constant<int, 0>{});
-#ifdef GO2PI_DIAG_CLOCK
-  if (st && wave == 0 && lane == 0) st[44] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP_AT(st, wave == 0 && lane == 0, 44);
   float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
@@ -1172,9 +937,7 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
     hn[i] = make_float4(o[0], o[1], o[2], o[3]);
     *reinterpret_cast<float4 *>(yrow + i * 16) = hn[i];
   }
-#ifdef GO2PI_DIAG_CLOCK
-  if (st && wave == 0 && lane == 0) st[45] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP_AT(st, wave == 0 && lane == 0, 45);
 }
 
 // LSTM cell as the pipeline's front stage (one wave per SIMD), the sibling of
@@ -1319,11 +1082,13 @@ struct W4Hot {
   int nbias, head_n, c0, hid_act, head_act;
   float hid_alpha, head_alpha;
   int post_plain;
+  float hid_beta, head_beta;
 };
 
 __device__ __forceinline__ W4Hot w4_hot(const DevProgram &P) {
   return W4Hot{P.l0_w,     P.head_w,  P.head_bias, P.bpack,    P.err_hot,   P.nbias,
-               P.head_n,   P.c0,      P.hid_act,   P.head_act, P.hid_alpha, P.head_alpha, P.post_plain};
+               P.head_n,   P.c0,      P.hid_act,   P.head_act, P.hid_alpha, P.head_alpha, P.post_plain,
+               P.hid_beta, P.head_beta};
 }
 
 // f(integral_constant<activation>): A >= 0 a compile-time activation (the lean
@@ -1408,21 +1173,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     hot.head_act = P.head_act;
     hot.hid_alpha = P.hid_alpha;
     hot.head_alpha = P.head_alpha;
+    hot.hid_beta = P.hid_beta;
+    hot.head_beta = P.head_beta;
   }
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 42] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP(P, threadIdx.x == 0 && step == 0, 42);
   // layer 0's input rows are complete in X0 and the biases in LDS (this wave's
   // direct-to-LDS loads, older than the ring's); the ring's loads stay in flight
   wg_barrier_vm<RD * TPW>();
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP(P, threadIdx.x == 0 && step == 0, 4);
   if constexpr (CTL) {
     if (ctl.status && (int)threadIdx.x < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + threadIdx.x] = CL.nanf[threadIdx.x];
-#ifdef GO2PI_DIAG_CLOCK
-    if (threadIdx.x == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, threadIdx.x == 0, 15);
   }
   // the head's fragments (final layer, fused): fetched before the last hidden layer's LDS phase
   float4 hw[HT][TPW];
@@ -1452,15 +1213,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       w4_lds_phase<TPW, RD, K0S, NT0, false>(X0, S, lane, hot.c0, 0, 0, ws, CSB, ws, 0, 0, 1, vo, acc, f);
     }
   }
-#ifdef GO2PI_DIAG_CLOCK  // pipeline stamps: 6 + l = wave 0 done with hidden layer l, 6 + nh = head barrier;
-                         // 16 + 3w + min(l, 2) = wave w done with hidden layer l
-  if (lane == 0 && P.stamps && step == 0) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave] = __builtin_amdgcn_s_memtime();
-    if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6] = __builtin_amdgcn_s_memtime();
-  }
-#endif
+  // pipeline stamps: 6 + l = wave 0 done with hidden layer l, 6 + nh = head barrier;
+  // 16 + 3w + min(l, 2) = wave w done with hidden layer l
+  GO2PI_STAMP(P, lane == 0 && step == 0, 16 + 3 * wave);
+  GO2PI_STAMP(P, lane == 0 && step == 0 && wave == 0, 6);
   float *Y = Y0;  // where the previous layer's activations go
-  const float alpha = hot.hid_alpha;
+  const float alpha = hot.hid_alpha, beta = hot.hid_beta;
 #pragma unroll(NHC > 0 ? NHC : 1)
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
@@ -1479,41 +1237,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile stores are in LDS
       if (lane == 0) __hip_atomic_store(flags + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-#ifdef GO2PI_DIAG_CLOCK  // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
-    unsigned long long *sub =
-        (lane == 0 && P.stamps && step == 0 && l == 1) ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG + 28 + 3 * wave
-                                                        : nullptr;
-#endif
-#ifdef GO2PI_DIAG_WEAVE
-    constexpr bool WEAVE = HO && !BIN;
-#else
-    constexpr bool WEAVE = false;
-#endif
-    if constexpr (WEAVE) {
-    // variant: layer l-1's epilogue of tile i+1 woven between layer l's MFMAs of
-    // chunk t0+i (register hand-off shapes only)
-    act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
-      constexpr int ACT = decltype(act_k)::value;
-      float4 v = w4_epi<ACT>(alpha, acc[0], bv[0]);
-      *reinterpret_cast<float4 *>(yrow) = v;
-      auto own = [&](auto i_k) {
-        constexpr int I = decltype(i_k)::value;
-        const int cl = (t0 + I + RD) & (CH - 1);  // chunk loaded into slot (I + RD) & 3
-        constexpr int IN = I + 1 < TPW ? I + 1 : I;
-        float4 vn = v;
-        w4_own_chunk<TPW, (I & 3), RD, ACT, (I + 1 < TPW)>(accn, f, v, ws, vo, cl * CSB, acc[IN], bv[IN], alpha,
-                                                           vn);
-        if constexpr (I + 1 < TPW) {
-          v = vn;
-          *reinterpret_cast<float4 *>(yrow + (I + 1) * 16) = v;
-        }
-      };
-      [&]<int... I>(std::integer_sequence<int, I...>) {
-        (own(std::integral_constant<int, I>{}), ...);
-      }(std::make_integer_sequence<int, TPW>{});
-    });
-    publish();
-    } else {
+    // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
+    [[maybe_unused]] const bool sub = lane == 0 && step == 0 && l == 1;
+    {
     // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
     // publish, then layer l's MFMAs over those chunks with the B operand from registers
     // (!HO: the epilogue to LDS, then a workgroup barrier)
@@ -1523,18 +1249,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if constexpr (ACTC == 1) v[i] = w4_epi_elu1<BIN>(acc[i], bv[i]);
-        else v[i] = w4_epi<ACT>(alpha, acc[i], bv[i]);
+        else v[i] = w4_epi<ACT>(alpha, beta, acc[i], bv[i]);
       }
 #pragma unroll
       for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
-#ifdef GO2PI_DIAG_CLOCK  // slot 46 + w: layer 1's epilogue issued (before the publish)
-      if (sub) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 46 + wave] = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef GO2PI_DIAG_LATEPUBALL  // variant (diagnostics): the late flag in the general body too
-      constexpr bool LATEPUB = HO;
-#else
+      GO2PI_STAMP(P, sub, 46 + wave);  // layer 1's epilogue issued (before the publish)
       constexpr bool LATEPUB = HO && PL;
-#endif
       if constexpr (LATEPUB) {
         // the lean kernel publishes after its first own chunk: the publish's
         // lgkmcnt(0) then finds the tile stores landed instead of holding the MFMAs
@@ -1555,13 +1275,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     });
     if constexpr (!HO) __syncthreads();
     }
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[0] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, sub, 28 + 3 * wave);
     if constexpr (HO) w4_wait(flags, wave, ep, lane, hot.err);
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[1] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, sub, 29 + 3 * wave);
     // LDS phase: the other waves' chunks, rotated order from t0 + TPW
     constexpr int K0 = HO ? TPW : 0;                             // first chunk index of the LDS phase
     constexpr int NT = (CH - K0) % 4 ? (CH - K0) % 4 : 4;       // chunks in the LDS phase's last group
@@ -1571,32 +1287,22 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       load_head();  // the head's fragments, behind the last LDS phase
       w4_lds_phase<TPW, RD, (K0 & 3), NT, false>(Y, S, lane, CH, kb1, K0, ws, CSB, wn, CSB, 0, 1, vo, accn, f);
     }
-#ifdef GO2PI_DIAG_CLOCK
-    if (sub) sub[2] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, sub, 30 + 3 * wave);
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       acc[i] = accn[i];
       bv[i] = bvn[i];
     }
     Y = Y == X0 ? Y0 : X0;
-#ifdef GO2PI_DIAG_CLOCK
-    if (lane == 0 && P.stamps && step == 0 && l < 8) {
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 16 + 3 * wave + (l < 3 ? l : 2)] = __builtin_amdgcn_s_memtime();
-      if (wave == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-    }
-#endif
+    GO2PI_STAMP(P, lane == 0 && step == 0 && l < 8, 16 + 3 * wave + (l < 3 ? l : 2));
+    GO2PI_STAMP(P, lane == 0 && step == 0 && l < 8 && wave == 0, 6 + l);
   }
   // the last hidden layer's epilogue feeds the head from registers (no LDS copy).
   // Four accumulator chains per head tile, one per k-step of a chunk, so that no
   // MFMA waits on the one before it (a single chain paid the dependent-accumulator
   // latency 4 x TPW times), summed in a fixed order: (c0 + c1) + (c2 + c3).
   {
-#ifdef GO2PI_DIAG_HEAD2  // variant (diagnostics): two chains (even / odd tiles)
-    constexpr int NCH = 2;
-#else
     constexpr int NCH = 4;
-#endif
     f32x4 hacc[HT][NCH];
 #pragma unroll
     for (int h = 0; h < HT; ++h)
@@ -1608,7 +1314,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       for (int i = 0; i < TPW; ++i) {
         float4 v;
         if constexpr (ACTC == 1) v = w4_epi_elu1<BIN>(acc[i], bv[i]);
-        else v = w4_epi<ACT>(alpha, acc[i], bv[i]);
+        else v = w4_epi<ACT>(alpha, beta, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
 #pragma unroll
@@ -1627,9 +1333,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     }
   }
   __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-  if (threadIdx.x == 0 && P.stamps && step == 0 && nh < 9) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + nh] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP(P, threadIdx.x == 0 && step == 0 && nh < 9, 6 + nh);
   if (wave < HT) {  // head tile `wave`: the four waves' partials in a fixed order, bias, final store
     f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
 #pragma unroll
@@ -1641,7 +1345,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
       with_act(hot.head_act, [&](auto act_k) {
         constexpr int ACT = decltype(act_k)::value;
-        const float4 v = w4_epi<ACT>(hot.head_alpha, hs[0], hbv[0]);
+        const float4 v = w4_epi<ACT>(hot.head_alpha, hot.head_beta, hs[0], hbv[0]);
         if (row < B) {  // (lean kernel: ac = the action rows of all steps, this step's at step * B
                         // rows; general body: ac = this step's rows already)
           float *o = ac + ((PL ? (size_t)step * B : (size_t)0) + row) * hot.head_n;
@@ -1678,10 +1382,11 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   // tell idle resident kernels on this device to give their CUs back (resident.hip)
-  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
+    __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)(dims >> 20);
   // (the program's fields are read inside w4_step once the first loads are out)
-  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f, 1};
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
   constexpr int S = 64 * TPW + 4;  // = P.lds_stride (the engine selects this kernel only then)
   float *bufA = lds, *bufB = lds + GO2PI_TILE_ROWS * S;
   f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + 2 * GO2PI_TILE_ROWS * S);
@@ -1705,23 +1410,15 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
                                          (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
     }
     if (step == 0 && tid < 4) flags[tid] = 0;
-#ifdef GO2PI_DIAG_CLOCK
-    if (tid == 0 && P.stamps && step == 0) {
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 1] = __builtin_amdgcn_s_memrealtime();
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 40] = __builtin_amdgcn_s_memtime();
-      P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
-    }
-#endif
+    GO2PI_STAMP(P, tid == 0 && step == 0, 0);
+    GO2PI_STAMP_RT(P, tid == 0 && step == 0, 1);
+    GO2PI_STAMP(P, tid == 0 && step == 0, 40);
+    GO2PI_STAMP(P, tid == 0 && step == 0, 41);
     w4_step<TPW, HT, false, true, C0M, ACTC, NHC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
                                        CtlLds{}, step);
   }
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 2] = __builtin_amdgcn_s_memtime();
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 3] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  GO2PI_STAMP(P, tid == 0, 2);
+  GO2PI_STAMP_RT(P, tid == 0, 3);
 }
 
 // RNN: the recurrent cell this instantiation runs when the program has one (0 GRU,
@@ -1742,12 +1439,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   constexpr int NT = NW * 64;
   // tell idle resident kernels on this device to give their CUs back (resident.hip)
-  if (blockIdx.x == 0 && tid == 0 && P.yield)
+  if (blockIdx.x == 0 && tid == 0 && P.yield && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(P.yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int H = P.gru.H, SW = P.gru.sw;  // hidden width; state floats per robot (LSTM: h | c)
-#ifdef GO2PI_DIAG_PRIO  // variant: static priority for the second-dispatched half of the waves
-  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   // Touch every layer descriptor up front: one burst of scalar loads warms the
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
@@ -1760,15 +1454,10 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     for (int l = 0; l < P.nl; ++l) d ^= P.L[l].K_pad ^ P.L[l].N_pad ^ P.L[l].act ^ (int)(size_t)P.L[l].w;
     asm volatile("" ::"s"(d));  // consumes the loads; no side effect
   }
-#ifdef GO2PI_DIAG_CLOCK  // init sub-phases: 40 descriptors warm, 41 observation loads issued, 42 pipeline barrier reached
-  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 40] = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 0] = __builtin_amdgcn_s_memtime();
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 1] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  // init sub-phases: 40 descriptors warm, 41 observation loads issued, 42 pipeline barrier reached
+  GO2PI_STAMP(P, tid == 0, 40);
+  GO2PI_STAMP(P, tid == 0, 0);
+  GO2PI_STAMP_RT(P, tid == 0, 1);
 
   // controller tick: this tile's raw inputs staged in LDS behind the scratch
   // region (one burst of direct-to-LDS loads), then assembled from there
@@ -1789,13 +1478,11 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
     lds_dma_wait();
     __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-    if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 5] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, tid == 0, 5);
   }
   // plain observation rows with no prologue arithmetic are staged by direct-to-LDS
   // loads (needs whole 64-column chunks to fit the LDS row)
-  const bool glds_obs = !CTL && !P.pre_sub && !P.pre_div && !(P.obs_clip > 0.f) && ((P.in_pad + 63) & ~63) <= S;
+  const bool glds_obs = !CTL && !P.pre_sub && !P.pre_div && !P.pre_mul && !P.pre_clip && ((P.in_pad + 63) & ~63) <= S;
   auto stage_obs = [&](int step) {
     if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
       if constexpr (NW == 4)
@@ -1846,9 +1533,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // next layer, so they must hold finite values: clear everything the
   // observation does not cover, once.
   stage_obs(0);
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 41] = __builtin_amdgcn_s_memtime();
-#endif
+  GO2PI_STAMP(P, tid == 0, 41);
   if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tail4 = (S - P.in_pad) >> 2;
@@ -1943,13 +1628,6 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         }
         X0 = bufB;
         Y0 = bufA;
-#ifdef GO2PI_DIAG_GRUDBG
-        __syncthreads();
-        if (blockIdx.x == 0 && tid < 2)
-          printf("tid %d x %g %g %g h0 %g %g h1 %g %g %g S %d H %d in_pad %d has_gru %d\n", tid, bufA[tid * S],
-                 bufA[tid * S + 1], bufA[tid * S + 47], bufH[tid * S], bufH[tid * S + 255], bufB[tid * S],
-                 bufB[tid * S + 1], bufB[tid * S + 255], S, H, P.in_pad, P.has_gru);
-#endif
       }
       w4_step<W4T, W4H, CTL, false, C0M, ACTC, NHC>(P, w4_hot(P), X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv,
                                          row0, B, ctl, CL,
@@ -1958,14 +1636,10 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     }
     lds_dma_wait();  // the observation tile's direct-to-LDS loads
     __syncthreads();
-#ifdef GO2PI_DIAG_CLOCK
-    if (tid == 0 && P.stamps && step == 0) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 4] = __builtin_amdgcn_s_memtime();
-#endif
+    GO2PI_STAMP(P, tid == 0 && step == 0, 4);
     if constexpr (CTL) {
       if (ctl.status && tid < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + tid] = CL.nanf[tid];
-#ifdef GO2PI_DIAG_CLOCK
-      if (tid == 0 && P.stamps) P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 15] = __builtin_amdgcn_s_memtime();
-#endif
+      GO2PI_STAMP(P, tid == 0, 15);
     }
     float *X = bufA, *Y = bufB;
     if (P.has_gru) {
@@ -1981,51 +1655,22 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       // no barrier needed: layer 0 below reads bufB (X) and writes bufA (Y); bufH is
       // next read after the end-of-step barrier
     }
-    Handoff hin{nullptr, 0, 1};  // layer input complete: the barrier above
     for (int l = 0; l < P.nl; ++l) {
       const bool last = l == P.nl - 1;
       if (P.head_fuse && l == P.nl - 2) {
         if (P.head_fuse == 1)
-          dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
-        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B, hin);
+          dense_layer_head<NW, 1>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
+        else dense_layer_head<NW, 2>(P, P.L[l], P.L[l + 1], X, Y, S, scratch, wave, lane, row0, B);
         __syncthreads();
         head_finish<NW>(P, P.L[l + 1], scratch, wave, lane, ac, cv, row0, B);
-#ifdef GO2PI_DIAG_CLOCK
-        if (tid == 0 && P.stamps && step == 0 && l < 8) {  // slots 6..14 (15 is the controller tick's)
-          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-          P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 7 + l] = __builtin_amdgcn_s_memtime();
-        }
-#endif
+        // slots 6..14 (15 is the controller tick's)
+        GO2PI_STAMP(P, tid == 0 && step == 0 && l < 8, 6 + l);
+        GO2PI_STAMP(P, tid == 0 && step == 0 && l < 8, 7 + l);
         break;  // scratch is next written two barriers later; bufA/bufB are free
       }
-      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B, hin);
-      // two wide layers in a row (both split by tiles over the waves, no split-K)
-      // hand off through per-wave flags instead of a workgroup barrier
-      const int T = P.L[l].N_pad >> 4;
-#ifdef GO2PI_DIAG_HANDOFF
-      // variant (diagnostics): flag hand-off between two wide layers. Measured
-      // slower than the barrier on MI355X (mlp512: 47.8 vs 45.6 us per launch;
-      // gru256: 78.4 vs 76.4 us), so the shipped build keeps the barrier.
-      const bool flag_next = !last && T >= NW && (P.L[l + 1].N_pad >> 4) >= NW;
-#else
-      const bool flag_next = false;  // a workgroup barrier after every layer
-#endif
-      if (flag_next) {
-        ++ep;
-        handoff_publish(flags, wave, lane, ep);
-        hin = Handoff{flags, ep, (T + NW - 1) / NW};
-        hin.err = P.err;
-      } else {
-        hin = Handoff{nullptr, 0, 1};
-#ifdef GO2PI_DIAG_PREFETCH  // variant (diagnostics): measured slower, see DESIGN §4.1
-        if (!last) prefetch_first<NW>(P.L[l + 1], wave, lane, hin);
-#endif
-        __syncthreads();
-      }
-#ifdef GO2PI_DIAG_CLOCK
-      if (tid == 0 && P.stamps && step == 0 && l < 9)  // slots 6..14 (15 is the controller tick's)
-        P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 6 + l] = __builtin_amdgcn_s_memtime();
-#endif
+      dense_layer<NW>(P, P.L[l], X, Y, S, scratch, wave, lane, last, ac, cv, row0, B);
+      __syncthreads();  // a workgroup barrier after every layer (dense_acc: flags measured slower)
+      GO2PI_STAMP(P, tid == 0 && step == 0 && l < 9, 6 + l);  // slots 6..14 (15 is the controller tick's)
       float *t = X;
       X = Y;
       Y = t;
@@ -2037,12 +1682,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       if (row < B) hidden[(size_t)row * SW + k] = bufH[r * S + k];
     }
   }
-#ifdef GO2PI_DIAG_CLOCK
-  if (tid == 0 && P.stamps) {
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 2] = __builtin_amdgcn_s_memtime();
-    P.stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + 3] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  GO2PI_STAMP(P, tid == 0, 2);
+  GO2PI_STAMP_RT(P, tid == 0, 3);
 }
 
 // W4T > 0: the 4-wave uniform-MLP pipeline with W4T tiles per wave and a W4H-tile

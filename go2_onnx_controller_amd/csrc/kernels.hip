@@ -106,7 +106,7 @@ __global__ __launch_bounds__(GEMV_WAVES * 64) void gemv_layer_kernel(DevProgram 
     for (int b = 0; b < B; ++b) {
       float s = 0.f;
       for (int w2 = 0; w2 < GEMV_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
-      float v = act_fn(L.act, L.alpha, s + bv);
+      float v = act_fn(L.act, L.alpha, L.beta, s + bv);
       if (last) {
         if (n < L.N) y[(size_t)b * y_stride + n] = post_fn(P, v);
       } else {
@@ -262,7 +262,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
       for (int b = 0; b < B; ++b) {
         float s = 0.f;
         for (int w2 = 0; w2 < LAT_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
-        const float v = act_fn(L.act, L.alpha, s + bv);
+        const float v = act_fn(L.act, L.alpha, L.beta, s + bv);
         if (last) {
           if (n < L.N) {
             if constexpr (CTL) ctl_store(cv, b, n, post_fn(P, v));

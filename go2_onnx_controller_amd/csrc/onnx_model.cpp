@@ -167,9 +167,10 @@ Tensor parse_tensor(Span s) {
 struct Attr {
   float f = 0.f;
   int64_t i = 0;
-  bool has_f = false, has_i = false;
+  bool has_f = false, has_i = false, has_t = false;
   std::vector<int64_t> ints;
   std::vector<float> floats;
+  Tensor t;  // AttributeProto.t (a Constant node's value)
 };
 
 struct Node {
@@ -205,6 +206,7 @@ Node parse_node(Span s) {
           if (g.no == 1) name = str(g.s);
           else if (g.no == 2) { a.f = as_f32(g.v); a.has_f = true; }
           else if (g.no == 3) { a.i = int64_t(g.v); a.has_i = true; }
+          else if (g.no == 5 && g.wt == 2) { a.t = parse_tensor(g.s); a.has_t = true; }
           else if (g.no == 7) {
             if (g.wt == 2) {
               size_t k = g.s.n / 4, o = a.floats.size();
@@ -261,7 +263,35 @@ int act_of(const std::string &op) {
   if (op == "Tanh") return ACT_TANH;
   if (op == "Sigmoid") return ACT_SIGMOID;
   if (op == "LeakyRelu") return ACT_LEAKY;
+  if (op == "Selu") return ACT_SELU;
+  if (op == "Softplus") return ACT_SOFTPLUS;
+  if (op == "HardSigmoid") return ACT_HARDSIGMOID;
+  if (op == "HardSwish") return ACT_HARDSWISH;
+  if (op == "Softsign") return ACT_SOFTSIGN;
   return -1;
+}
+
+// The node's attributes with the ONNX defaults (opset 6+ for Elu / LeakyRelu /
+// Selu / HardSigmoid, opset 14 HardSwish: alpha = 1/6, beta = 0.5 fixed).
+void act_attrs(const Node &nd, int act, float &alpha, float &beta) {
+  alpha = beta = 0.f;
+  switch (act) {
+    case ACT_ELU: alpha = nd.fattr("alpha", 1.f); break;
+    case ACT_LEAKY: alpha = nd.fattr("alpha", 0.01f); break;
+    case ACT_SELU:
+      alpha = nd.fattr("alpha", 1.67326319217681884765625f);
+      beta = nd.fattr("gamma", 1.05070102214813232421875f);
+      break;
+    case ACT_HARDSIGMOID:
+      alpha = nd.fattr("alpha", 0.2f);
+      beta = nd.fattr("beta", 0.5f);
+      break;
+    case ACT_HARDSWISH:
+      alpha = 1.f / 6.f;
+      beta = 0.5f;
+      break;
+    default: break;
+  }
 }
 
 }  // namespace
@@ -303,6 +333,22 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       else if (f.no == 12) m.outputs.push_back(parse_value_info(f.s));
     }
   }
+  // Constant nodes (torch.onnx.export writes scalars such as a Clip bound or a Mul
+  // factor this way) become initializers of their output
+  for (auto &nd : nodes) {
+    if (nd.op != "Constant" || nd.out.empty()) continue;
+    Tensor t;
+    auto it = nd.attrs.find("value");
+    if (it != nd.attrs.end() && it->second.has_t) t = it->second.t;
+    else if ((it = nd.attrs.find("value_float")) != nd.attrs.end()) { t.dtype = 1; t.f = {it->second.f}; }
+    else if ((it = nd.attrs.find("value_floats")) != nd.attrs.end()) {
+      t.dtype = 1;
+      t.f = it->second.floats;
+      t.dims = {int64_t(t.f.size())};
+    } else fail("Constant node '" + nd.name + "' without a value");
+    t.name = nd.out[0];
+    inits[t.name] = std::move(t);
+  }
   for (auto &io : raw_inputs)
     if (!inits.count(io.name)) m.inputs.push_back(io);
   if (m.inputs.empty() || m.outputs.empty()) fail("graph needs at least one input and one output");
@@ -325,7 +371,36 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   std::vector<bool> used(nodes.size(), false);
   bool last_has_act = true;  // true => next Add cannot fold into a bias
   bool pending_bias_ok = false;
+  // elementwise ops after the last layer's activation: a Mul by a constant is held
+  // here (col_scale) and folded into the next Gemm's input columns; at the end of
+  // the graph a scalar one becomes post_scale, and a Clip becomes the output clip
+  std::vector<float> col_scale;
+  bool post_clip = false;
+  size_t rnn_node = SIZE_MAX;  // the recurrent cell's node
   const std::string &final_out = m.outputs[0].name;
+  auto const_vec = [&](const Tensor &C, int n, const std::string &what) {
+    if (C.numel() != n && C.numel() != 1) fail(what + " must broadcast over " + std::to_string(n) + " features");
+    std::vector<float> v(n);
+    for (int i = 0; i < n; ++i) v[i] = C.numel() == 1 ? C.f[0] : C.f[i];
+    return v;
+  };
+  auto scalar_of = [&](const std::string &name) -> float {
+    const Tensor &t = init(name);
+    if (t.f.empty()) fail("'" + name + "' is empty");
+    if (t.numel() != 1) fail("'" + name + "' must be a scalar");
+    return t.f[0];
+  };
+  // a new linear layer: no trailing op may sit between it and the previous one,
+  // except a held column scale, folded into its weights here
+  auto begin_layer = [&](Dense &d, const std::string &op) {
+    if (post_clip) fail(op + ": a Clip after an activation is only supported at the end of the graph");
+    if (!col_scale.empty()) {
+      if ((int)col_scale.size() != 1 && (int)col_scale.size() != d.K) fail(op + ": the Mul before it must broadcast over K");
+      for (int i = 0; i < d.N; ++i)
+        for (int k = 0; k < d.K; ++k) d.W[size_t(i) * d.K + k] *= col_scale[col_scale.size() == 1 ? 0 : k];
+      col_scale.clear();
+    }
+  };
   while (cur != final_out) {
     auto it = consumers.find(cur);
     size_t idx = SIZE_MAX;
@@ -339,6 +414,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       if (nd.in.size() < 2) fail(nd.op + " needs two inputs");
       return nd.in[0] == cur ? nd.in[1] : nd.in[0];
     };
+    const bool at_input = m.layers.empty() && !m.has_gru;  // still in front of the first layer
 
     if (nd.op == "Gemm") {
       if (nd.in[0] != cur) fail("Gemm: activation must be input A");
@@ -365,6 +441,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
           d.b[i] = beta == 1.f ? c : beta * c;
         }
       }
+      begin_layer(d, "Gemm");
       m.layers.push_back(std::move(d));
       last_has_act = false;
       pending_bias_ok = true;
@@ -379,6 +456,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       for (int i = 0; i < d.N; ++i)
         for (int k = 0; k < d.K; ++k) d.W[size_t(i) * d.K + k] = B.f[size_t(k) * d.N + i];
       d.b.assign(d.N, 0.f);
+      begin_layer(d, "MatMul");
       m.layers.push_back(std::move(d));
       last_has_act = false;
       pending_bias_ok = true;
@@ -388,28 +466,76 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       Dense &d = m.layers.back();
       if (C.numel() != d.N && C.numel() != 1) fail("Add: bias must broadcast over N");
       for (int i = 0; i < d.N; ++i) d.b[i] += C.numel() == 1 ? C.f[0] : C.f[i];
-    } else if ((nd.op == "Sub" || nd.op == "Div") && is_init(other_input()) && nd.in[0] == cur &&
-               m.layers.empty() && !m.has_gru) {
+    } else if ((nd.op == "Sub" || nd.op == "Div") && at_input && nd.in[0] == cur && is_init(other_input())) {
+      // observation normalisation, evaluated as written: (x - sub) / div
       const Tensor &C = init(other_input());
       std::vector<float> &dst = nd.op == "Sub" ? m.pre_sub : m.pre_div;
       if (!dst.empty()) fail("only one " + nd.op + " in the prologue is supported");
-      if (nd.op == "Sub" && !m.pre_div.empty()) fail("prologue must be Sub then Div");
+      if (nd.op == "Sub" && (!m.pre_div.empty() || !m.pre_mul.empty())) fail("prologue must be Sub, then Div / Mul");
+      if (!m.pre_mul.empty() || std::isfinite(m.pre_lo) || std::isfinite(m.pre_hi))
+        fail("prologue must be Sub, Div, Mul, then Clip");
       dst = C.f;
+    } else if (nd.op == "Mul" && at_input && is_init(other_input())) {
+      if (!m.pre_mul.empty()) fail("only one Mul in the prologue is supported");
+      if (std::isfinite(m.pre_lo) || std::isfinite(m.pre_hi)) fail("prologue must be Sub, Div, Mul, then Clip");
+      m.pre_mul = init(other_input()).f;
+    } else if ((nd.op == "Mul" || (nd.op == "Div" && nd.in[0] == cur)) && is_init(other_input())) {
+      // a constant scale between or after the layers (its reciprocal for a Div)
+      const Tensor &C = init(other_input());
+      if (m.has_gru && m.layers.empty()) fail(nd.op + " right after the recurrent cell is unsupported");
+      if (post_clip && C.numel() != 1) fail("a per-feature " + nd.op + " after the output Clip is unsupported");
+      const bool div = nd.op == "Div";
+      if (!last_has_act) {
+        // straight after Gemm (+ bias): scale the layer's rows and bias
+        Dense &d = m.layers.back();
+        const std::vector<float> sc = const_vec(C, d.N, nd.op);
+        for (int i = 0; i < d.N; ++i) {
+          const float f = div ? 1.f / sc[i] : sc[i];
+          for (int k = 0; k < d.K; ++k) d.W[size_t(i) * d.K + k] *= f;
+          d.b[i] *= f;
+        }
+      } else {
+        // after an activation: held for the next layer's input columns (or the output)
+        const int n = m.layers.back().N;
+        std::vector<float> sc = const_vec(C, n, nd.op);
+        if (C.numel() == 1) sc.resize(1);
+        for (auto &v : sc) v = div ? 1.f / v : v;
+        if (col_scale.empty()) col_scale = sc;
+        else if (col_scale.size() == 1 && sc.size() == 1) col_scale[0] *= sc[0];
+        else fail("two vector Mul / Div in a row are unsupported");
+      }
+    } else if (nd.op == "Clip") {
+      // opset >= 11: min/max are optional inputs; opset 6: attributes
+      float lo = nd.fattr("min", -INFINITY), hi = nd.fattr("max", INFINITY);
+      if (nd.in.size() > 1 && !nd.in[1].empty()) lo = scalar_of(nd.in[1]);
+      if (nd.in.size() > 2 && !nd.in[2].empty()) hi = scalar_of(nd.in[2]);
+      if (at_input) {
+        // clip of the observation (after any normalisation)
+        m.pre_lo = std::max(m.pre_lo, lo);
+        m.pre_hi = std::min(m.pre_hi, hi);
+      } else if (m.has_gru && m.layers.empty()) {
+        fail("Clip right after the recurrent cell is unsupported");
+      } else if (!last_has_act) {
+        // the layer's activation (ReLU6 = Clip(0, 6)), applied in its epilogue
+        Dense &d = m.layers.back();
+        d.act = ACT_CLIP;
+        d.alpha = lo;
+        d.beta = hi;
+        last_has_act = true;
+        pending_bias_ok = false;
+      } else {
+        // after an activation: only as the output clip (the action epilogue)
+        if (!col_scale.empty()) fail("Clip after a Mul that follows an activation is unsupported");
+        m.clip_lo = std::max(m.clip_lo, lo);
+        m.clip_hi = std::min(m.clip_hi, hi);
+        post_clip = true;
+      }
     } else if (act_of(nd.op) >= 0) {
       if (m.layers.empty()) fail(nd.op + " before any linear layer");
       if (last_has_act) fail("two activations in a row are unsupported");
       Dense &d = m.layers.back();
       d.act = act_of(nd.op);
-      d.alpha = nd.op == "Elu" ? nd.fattr("alpha", 1.f) : (nd.op == "LeakyRelu" ? nd.fattr("alpha", 0.01f) : 0.f);
-      last_has_act = true;
-      pending_bias_ok = false;
-    } else if (nd.op == "Clip") {
-      // opset >= 11: min/max are optional inputs; opset 6: attributes
-      float lo = nd.fattr("min", -INFINITY), hi = nd.fattr("max", INFINITY);
-      if (nd.in.size() > 1 && !nd.in[1].empty()) lo = init(nd.in[1]).f.at(0);
-      if (nd.in.size() > 2 && !nd.in[2].empty()) hi = init(nd.in[2]).f.at(0);
-      m.clip_lo = std::max(m.clip_lo, lo);
-      m.clip_hi = std::min(m.clip_hi, hi);
+      act_attrs(nd, d.act, d.alpha, d.beta);
       last_has_act = true;
       pending_bias_ok = false;
     } else if (nd.op == "Identity" || nd.op == "Flatten") {
@@ -457,6 +583,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       if (lstm && nd.in.size() > 7 && !nd.in[7].empty()) fail("LSTM: peepholes (input P) unsupported");
       m.gru = std::move(g);
       m.has_gru = true;
+      rnn_node = idx;
       // follow Y_h (output 1) if consumed, else Y (output 0)
       std::string next;
       if (nd.out.size() > 1 && !nd.out[1].empty() && consumers.count(nd.out[1])) next = nd.out[1];
@@ -475,6 +602,70 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   }
 
   if (m.layers.empty()) fail("policy has no linear layer");
+  if (rnn_node != SIZE_MAX) {
+    // The recurrent state I/O listed as (h, c) after the observation / action, whatever
+    // the graph's order: traced by name to the cell's initial_h / initial_c (inputs 5,
+    // 6) through Unsqueeze / Identity / Reshape, and Y_h / Y_c (outputs 1, 2) through
+    // Squeeze / Identity / Reshape. Other extra graph inputs / outputs keep their order.
+    const Node &cell = nodes[rnn_node];
+    auto producer = [&](const std::string &v) -> const Node * {
+      for (auto &nd : nodes)
+        for (auto &o : nd.out)
+          if (o == v) return &nd;
+      return nullptr;
+    };
+    auto is_pass = [](const std::string &op, bool in) {
+      return op == "Identity" || op == "Reshape" || op == (in ? "Unsqueeze" : "Squeeze");
+    };
+    auto find_io = [](std::vector<IoInfo> &v, const std::string &name) -> long {
+      for (size_t i = 1; i < v.size(); ++i)
+        if (v[i].name == name) return (long)i;
+      return -1;
+    };
+    auto trace_in = [&](size_t k) -> long {
+      if (cell.in.size() <= k || cell.in[k].empty()) return -1;
+      std::string v = cell.in[k];
+      for (int hop = 0; hop < 8; ++hop) {
+        const long i = find_io(m.inputs, v);
+        if (i >= 0) return i;
+        const Node *pr = producer(v);
+        if (!pr || !is_pass(pr->op, true) || pr->in.empty()) return -1;
+        v = pr->in[0];
+      }
+      return -1;
+    };
+    auto trace_out = [&](size_t k) -> long {
+      if (cell.out.size() <= k || cell.out[k].empty()) return -1;
+      std::string v = cell.out[k];
+      for (int hop = 0; hop < 8; ++hop) {
+        const long i = find_io(m.outputs, v);
+        if (i >= 0) return i;
+        auto ci = consumers.find(v);
+        if (ci == consumers.end()) return -1;
+        const Node *nx = nullptr;
+        for (size_t c : ci->second)
+          if (is_pass(nodes[c].op, false)) nx = &nodes[c];
+        if (!nx || nx->out.empty()) return -1;
+        v = nx->out[0];
+      }
+      return -1;
+    };
+    auto reorder = [](std::vector<IoInfo> &v, long h, long c) {
+      std::vector<IoInfo> r{v[0]};
+      if (h > 0) r.push_back(v[h]);
+      if (c > 0) r.push_back(v[c]);
+      for (long i = 1; i < (long)v.size(); ++i)
+        if (i != h && i != c) r.push_back(v[i]);
+      v = std::move(r);
+    };
+    const bool lstm = m.gru.cell == 1;
+    reorder(m.inputs, trace_in(5), lstm ? trace_in(6) : -1);
+    reorder(m.outputs, trace_out(1), lstm ? trace_out(2) : -1);
+  }
+  if (!col_scale.empty()) {
+    if (col_scale.size() != 1) fail("a per-feature Mul after the final activation is unsupported");
+    m.post_scale = col_scale[0];
+  }
   const int first_in = m.has_gru ? m.gru.I : m.layers[0].K;
   m.in_dim = first_in;
   if (m.has_gru && m.layers[0].K != m.gru.H) fail("recurrent hidden size does not match the first dense layer");
@@ -483,6 +674,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   m.out_dim = m.layers.back().N;
   if (!m.pre_sub.empty() && int(m.pre_sub.size()) != m.in_dim && m.pre_sub.size() != 1) fail("prologue Sub size");
   if (!m.pre_div.empty() && int(m.pre_div.size()) != m.in_dim && m.pre_div.size() != 1) fail("prologue Div size");
+  if (!m.pre_mul.empty() && int(m.pre_mul.size()) != m.in_dim && m.pre_mul.size() != 1) fail("prologue Mul size");
   // check declared feature dims against the program (reference reads shape.at(1), onnx_actor.cpp:32,35)
   const auto &is = m.inputs[0].shape, &os = m.outputs[0].shape;
   if (is.size() >= 2 && is[1] > 0 && is[1] != m.in_dim) fail("input feature dim disagrees with weights");

@@ -13,14 +13,21 @@
 
 namespace go2pi {
 
-enum Act : int { ACT_NONE = 0, ACT_ELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4, ACT_LEAKY = 5 };
+// The activation fused into a dense layer's epilogue (device_fn.hpp act_t), with
+// the ONNX node's attributes in alpha / beta: Elu / LeakyRelu alpha; Clip min / max
+// (a Clip right after a Gemm, e.g. ReLU6); Selu alpha / gamma; HardSigmoid and
+// HardSwish alpha / beta.
+enum Act : int {
+  ACT_NONE = 0, ACT_ELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4, ACT_LEAKY = 5,
+  ACT_CLIP = 6, ACT_SELU = 7, ACT_SOFTPLUS = 8, ACT_HARDSIGMOID = 9, ACT_HARDSWISH = 10, ACT_SOFTSIGN = 11
+};
 
 struct Dense {
   int K = 0, N = 0;
   std::vector<float> W;  // [N][K] row-major (ONNX Gemm transB=1 layout)
   std::vector<float> b;  // [N]
   int act = ACT_NONE;
-  float alpha = 0.f;
+  float alpha = 0.f, beta = 0.f;
 };
 
 // ONNX GRU (opset 14), forward, layout 0, one layer; gates ordered z, r, h.
@@ -47,12 +54,18 @@ struct Model {
   std::string producer;
 
   // program
-  std::vector<float> pre_sub, pre_div;  // optional prologue (x - sub) / div, [in_dim]
+  // optional prologue clip((x - sub) / div * mul, pre_lo, pre_hi), each [in_dim] or [1]
+  std::vector<float> pre_sub, pre_div, pre_mul;
+  float pre_lo = -std::numeric_limits<float>::infinity();
+  float pre_hi = std::numeric_limits<float>::infinity();
   bool has_gru = false;
   Gru gru;
   std::vector<Dense> layers;
+  // after the final layer's activation: y <- post_scale * clip(y, clip_lo, clip_hi)
+  // (a trailing Clip and / or scalar Mul of the graph)
   float clip_lo = -std::numeric_limits<float>::infinity();
   float clip_hi = std::numeric_limits<float>::infinity();
+  float post_scale = 1.f;
   int in_dim = 0, out_dim = 0;
 };
 

@@ -22,6 +22,12 @@
 #define GO2PI_TILE_ROWS 16      // robots per workgroup tile in the batched kernel
 #define GO2PI_SMALL_MAXB 8      // max rows of the GEMV chain
 #define GO2PI_STAMPS_PER_WG 64  // diagnostics: {start,end} x {memtime,realtime}, phase marks, per-wave layer-1 marks
+// A batched launch of more than this many workgroups (one per CU: ~100 KiB of LDS
+// each) bumps the device's yield counter, so idle resident kernels (<= 32 CUs for the
+// 48->512^3->12 policy, 8 for the shipped one) give their CUs back; smaller launches
+// (a per-tick recurrent or controller launch at a few robots) fit beside them and
+// must not evict them on every call.
+#define GO2PI_YIELD_MIN_GRID 64
 
 namespace go2pi {
 
@@ -30,8 +36,8 @@ struct DevLayer {
   const float *bias;  // [N_pad], zero padded
   int K_pad, N_pad, N;
   int act;
-  float alpha;
-  int pad0, pad1, pad2;
+  float alpha, beta;  // the activation's attributes (onnx_model.hpp Dense)
+  int pad1, pad2;
 };
 
 // The recurrent cell in front of the dense head (ONNX GRU or LSTM; the field
@@ -77,11 +83,14 @@ struct DevProgram {
   int w4_c0m;             // pipeline: layer 0's k-chunks mod 4 (0 or 3; K padded to 16, not 64, when 3)
   int w4_actc;            // lean kernel: the hidden activation as a compile-time constant (1 = Elu), or -1
   int w4_nhc;             // lean kernel: the hidden-layer count as a compile-time constant (3), or 0 (runtime)
-  // prologue: x <- clamp((x - sub) / div, -obs_clip, obs_clip); sub/div may be null
+  float hid_beta, head_beta;  // second activation attribute of the hidden layers / the head (Clip max, ...)
+  // prologue: x <- clamp((x - sub) / div * mul, -obs_clip, obs_clip); sub/div/mul may be null
   const float *pre_sub;
   const float *pre_div;
-  int pre_sub_bcast, pre_div_bcast;  // 1: single scalar broadcast over features
-  float obs_clip;                    // <= 0: off
+  const float *pre_mul;
+  int pre_sub_bcast, pre_div_bcast, pre_mul_bcast;  // 1: single scalar broadcast over features
+  int pre_clip;         // 1: x <- clip(x, obs_lo, obs_hi) (a graph's input Clip and / or go2pi_opts.obs_clip)
+  float obs_lo, obs_hi;
   // epilogue on the final layer: y <- scale * clamp(tanh?(act(y)), lo, hi)
   int post_tanh;
   float clip_lo, clip_hi, scale;

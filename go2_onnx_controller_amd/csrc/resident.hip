@@ -220,7 +220,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
       acc = fmaf(a.w, w0[f].w, acc);
     }
     if (KS == 1) {
-      xs[b * K1 + n] = act_fn(L.act, L.alpha, acc + b0);
+      xs[b * K1 + n] = act_fn(L.act, L.alpha, L.beta, acc + b0);
     } else {
       p0[(ks * GO2PI_SMALL_MAXB + b) * N0 + n] = acc;
     }
@@ -231,7 +231,7 @@ __device__ __forceinline__ void local_layer0(const DevProgram &P, const float4 (
       const int b = i / N0, nn = i - b * N0;
       float acc = 0.f;
       for (int s2 = 0; s2 < KS; ++s2) acc += p0[(s2 * GO2PI_SMALL_MAXB + b) * N0 + nn];
-      xs[b * K1 + nn] = act_fn(L.act, L.alpha, acc + L.bias[nn]);
+      xs[b * K1 + nn] = act_fn(L.act, L.alpha, L.beta, acc + L.bias[nn]);
     }
   }
   lds_barrier();
@@ -311,6 +311,11 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   unsigned *lb = le + GO2PI_SMALL_MAXB;                   // [B] the granule buffer holding each row's h
   float *hown = reinterpret_cast<float *>(lb + GO2PI_SMALL_MAXB);  // [B][16] this workgroup's units' latest h'
   float *cown = hown + GO2PI_SMALL_MAXB * 16;             // LSTM: [B][16] its units' cell state
+  // the cell's outputs of the request in flight, copied to hown / cown only once this
+  // workgroup has finished the request: a request abandoned mid-layers (a sweep met a
+  // LEAVE tag) then leaves the committed state, which the leave path writes back, as it was
+  float *hst = cown + GO2PI_SMALL_MAXB * 16;              // [B][16]
+  float *cst = hst + GO2PI_SMALL_MAXB * 16;               // LSTM: [B][16]
   const size_t hbuf = (size_t)GO2PI_SMALL_MAXB * Hh;      // granules per buffer
   float4 wgf[RES_GS][NG];                                 // this workgroup's gate fragments (chunks wave + 8s)
   float gb[4] = {0.f, 0.f, 0.f, 0.f};                     // its biases: GRU z, r (summed), Wb_h, Rb_h; LSTM i, o, f, c
@@ -558,14 +563,14 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
                 // c: this workgroup's LDS copy once the row ran in this launch, else the state row
                 const float c_old = le[b] != 0u ? cown[b * 16 + lane] : hidden[(size_t)b * SW + Hh + j];
                 const float c_new = fg * c_old + ig * cg;
-                cown[b * 16 + lane] = c_new;
+                cst[b * 16 + lane] = c_new;
                 hnew = og * (2.f * sigmoid_fast(2.f * c_new) - 1.f);
               } else {
                 const float zg = sigmoid_fast(q[0]), rg = sigmoid_fast(q[1]);
                 const float hv = 2.f * sigmoid_fast(2.f * (q[2] + rg * q[3])) - 1.f;  // tanh, ~1e-7 abs
                 hnew = (1.f - zg) * hv + zg * hx[b * Kg + Ip + j];
               }
-              hown[b * 16 + lane] = hnew;
+              hst[b * 16 + lane] = hnew;
               __hip_atomic_store(hgran + (1u - lb[b]) * hbuf + (size_t)b * Hh + j, ((u64)e << 32) | __float_as_uint(hnew),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -660,7 +665,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         for (int b = 0; b < B; ++b) {
           float s = 0.f;
           for (int w2 = 0; w2 < RES_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
-          const float v = act_fn(L.act, L.alpha, s + bcur);
+          const float v = act_fn(L.act, L.alpha, L.beta, s + bcur);
           if (lastl) {
             if constexpr (CTL) {
               if (n < L.N) ctl_store(cv, b, n, post_fn(P, v));
@@ -689,6 +694,10 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       if (tid < B) {
         le[tid] = e;
         lb[tid] = 1u - lb[tid];
+      }
+      if (g < Ht && tid < B * 16) {  // this workgroup's units: the request is committed
+        hown[tid] = hst[tid];
+        if constexpr (LSTM) cown[tid] = cst[tid];
       }
     }
     if constexpr (CTL) {
@@ -761,7 +770,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   if (ctl) tail = (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
   if (rnn)
     tail = (size_t)GO2PI_SMALL_MAXB * (p.gru.I_pad + p.gru.H) + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16 +
-           2 * GO2PI_SMALL_MAXB + GO2PI_SMALL_MAXB * 16 * (lstm ? 2 : 1);
+           2 * GO2PI_SMALL_MAXB + 2 * GO2PI_SMALL_MAXB * 16 * (lstm ? 2 : 1);  // hown (cown), hst (cst)
   const size_t lds = sizeof(float) * (ctl_off + tail);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {

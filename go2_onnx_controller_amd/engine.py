@@ -199,7 +199,9 @@ class Engine:
         c = Cost()
         _check(L.go2pi_get_cost(h, ctypes.byref(c)))
         self.cost = {"flops_per_row": c.flops_per_row, "weight_bytes": c.weight_bytes,
-                     "io_bytes_per_row": c.io_bytes_per_row, "n_layers": c.n_layers, "has_gru": bool(c.has_gru)}
+                     "io_bytes_per_row": c.io_bytes_per_row, "n_layers": c.n_layers, "has_gru": bool(c.has_gru),
+                     "cell": {0: None, 1: "GRU", 2: "LSTM"}.get(c.has_gru)}
+        # recurrent state per robot: GRU h [H]; LSTM h [H] | c [H] (hidden_dim = their sum)
         self.batched_kernel = "unknown"
         if hasattr(L, "go2pi_batched_kernel") and L.go2pi_batched_kernel.argtypes:
             kb = ctypes.create_string_buffer(128)

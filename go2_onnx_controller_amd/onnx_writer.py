@@ -58,6 +58,11 @@ def attr_ints(name: str, ints) -> bytes:
     return f_str(1, name) + b"".join(f_varint(8, int(i)) for i in ints) + f_varint(20, 7)
 
 
+def attr_tensor(name: str, arr: np.ndarray) -> bytes:
+    """A TENSOR attribute (e.g. a Constant node's value)."""
+    return f_str(1, name) + f_bytes(5, tensor("", arr)) + f_varint(20, 4)
+
+
 def node(op: str, inputs, outputs, name: str = "", attrs=()) -> bytes:
     body = b"".join(f_str(1, i) for i in inputs)
     body += b"".join(f_str(2, o) for o in outputs)

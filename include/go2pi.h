@@ -122,7 +122,7 @@ typedef struct go2pi_cost {
   double weight_bytes;     /* fp32 parameter bytes (unpadded) */
   double io_bytes_per_row; /* obs + action (+ 2x hidden for recurrent) bytes */
   int32_t n_layers;
-  int32_t has_gru;
+  int32_t has_gru;         /* recurrent cell in front of the dense layers: 0 none, 1 GRU, 2 LSTM */
 } go2pi_cost;
 int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
 

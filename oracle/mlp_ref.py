@@ -6,7 +6,8 @@ unpinned — see oracle/onnx_ref.py.
 
 `mlp_layers(graph)` recognises the reference graph pattern
 (`onnx_inference/data/model.onnx`: Gemm(transB=1) -> Elu -> ... -> Gemm) and
-the MatMul+Add / Relu / Tanh / Sigmoid / LeakyRelu variants, independently of
+the MatMul+Add / Relu / Tanh / Sigmoid / LeakyRelu / Clip / Selu / Softplus /
+HardSigmoid / HardSwish / Softsign / constant-Mul variants, independently of
 the product's C++ pattern matcher.
 """
 from __future__ import annotations
@@ -49,43 +50,97 @@ def lib():
     return _lib
 
 
+ACT_DEFAULTS = {  # ONNX attribute defaults (alpha, beta) per activation
+    "Elu": (1.0, 0.0), "LeakyRelu": (0.01, 0.0), "Selu": (1.67326319217681884765625, 1.05070102214813232421875),
+    "HardSigmoid": (0.2, 0.5), "HardSwish": (1.0 / 6.0, 0.5), "Relu": (0.0, 0.0), "Tanh": (0.0, 0.0),
+    "Sigmoid": (0.0, 0.0), "Softplus": (0.0, 0.0), "Softsign": (0.0, 0.0)}
+
+
 def mlp_layers(g: onnx_ref.Graph):
-    """Return [(W[N,K] f32, b[N] f32, act_name, alpha)] for a Linear/act chain."""
+    """Return [(W[N,K] f32, b[N] f32, act_name, alpha, beta)] for a Linear/act chain.
+
+    Lowering rules (the ONNX semantics, restated independently of the product's
+    C++ matcher): a Clip right after a Gemm is that layer's activation (alpha =
+    min, beta = max); a constant Mul / Div right after a Gemm scales the layer's
+    rows and bias; one after an activation scales the next layer's input columns
+    (fp32 products in graph order). Prologue / output elementwise ops are not
+    layers (onnx_ref.act evaluates them)."""
     layers = []
     cur = g.inputs[0][0]
     producers = {}
+    consts = dict(g.inits)
     for nd in g.nodes:
+        if nd.op_type == "Constant":
+            v = nd.attrs.get("value")
+            consts[nd.outputs[0]] = np.asarray(v if v is not None else nd.attrs.get("value_float",
+                                                                                   nd.attrs.get("value_floats")),
+                                               np.float32)
         for i in nd.inputs:
             producers.setdefault(i, []).append(nd)
     consumed = set()
+    last_act = True
+    col_scale = None
+
+    def const_of(name):
+        return np.asarray(consts[name], np.float32)
+
     while True:
         nds = [n for n in producers.get(cur, []) if id(n) not in consumed]
         if not nds:
             break
         nd = nds[0]
         consumed.add(id(nd))
-        if nd.op_type == "Gemm":
-            W = g.inits[nd.inputs[1]].astype(np.float32)
-            if not nd.attrs.get("transB", 0):
-                W = W.T
-            W = W * np.float32(nd.attrs.get("alpha", 1.0))
-            b = g.inits[nd.inputs[2]].astype(np.float32) * np.float32(nd.attrs.get("beta", 1.0)) \
-                if len(nd.inputs) > 2 else np.zeros(W.shape[0], np.float32)
-            layers.append([np.ascontiguousarray(W), np.ascontiguousarray(b), "none", 0.0])
-        elif nd.op_type == "MatMul":
-            W = g.inits[nd.inputs[1]].astype(np.float32).T
-            layers.append([np.ascontiguousarray(W), np.zeros(W.shape[0], np.float32), "none", 0.0])
-        elif nd.op_type == "Add":
+        op = nd.op_type
+        if op in ("Gemm", "MatMul"):
+            if op == "Gemm":
+                W = g.inits[nd.inputs[1]].astype(np.float32)
+                if not nd.attrs.get("transB", 0):
+                    W = W.T
+                W = W * np.float32(nd.attrs.get("alpha", 1.0))
+                b = g.inits[nd.inputs[2]].astype(np.float32) * np.float32(nd.attrs.get("beta", 1.0)) \
+                    if len(nd.inputs) > 2 else np.zeros(W.shape[0], np.float32)
+                b = np.broadcast_to(b, (W.shape[0],)).astype(np.float32)
+            else:
+                W = g.inits[nd.inputs[1]].astype(np.float32).T
+                b = np.zeros(W.shape[0], np.float32)
+            if col_scale is not None:
+                W = W * np.broadcast_to(col_scale, (W.shape[1],))[None, :]
+                col_scale = None
+            layers.append([np.ascontiguousarray(W, np.float32), np.ascontiguousarray(b), "none", 0.0, 0.0])
+            last_act = False
+        elif op == "Add":
             other = nd.inputs[1] if nd.inputs[0] == cur else nd.inputs[0]
-            layers[-1][1] = layers[-1][1] + g.inits[other].astype(np.float32)
-        elif nd.op_type in ("Elu", "Relu", "Tanh", "Sigmoid", "LeakyRelu"):
-            default = {"Elu": 1.0, "LeakyRelu": 0.01}.get(nd.op_type, 0.0)
-            layers[-1][2] = nd.op_type
-            layers[-1][3] = float(nd.attrs.get("alpha", default))
-        elif nd.op_type in ("Sub", "Div", "Clip", "Identity", "Flatten"):
+            layers[-1][1] = layers[-1][1] + const_of(other)
+        elif op in ("Mul", "Div") and layers:
+            other = nd.inputs[1] if nd.inputs[0] == cur else nd.inputs[0]
+            f = const_of(other).reshape(-1)
+            if op == "Div":
+                f = np.float32(1.0) / f
+            if not last_act:
+                f = np.broadcast_to(f, (layers[-1][0].shape[0],))
+                layers[-1][0] = layers[-1][0] * f[:, None]
+                layers[-1][1] = layers[-1][1] * f
+            else:
+                col_scale = f if col_scale is None else col_scale * f
+        elif op == "Clip" and layers and not last_act:
+            lo = float(const_of(nd.inputs[1]).reshape(-1)[0]) if len(nd.inputs) > 1 and nd.inputs[1] else nd.attrs.get("min", -np.inf)
+            hi = float(const_of(nd.inputs[2]).reshape(-1)[0]) if len(nd.inputs) > 2 and nd.inputs[2] else nd.attrs.get("max", np.inf)
+            layers[-1][2:5] = ["Clip", float(np.float32(lo)), float(np.float32(hi))]
+            last_act = True
+        elif op in ACT_DEFAULTS:
+            da, db = ACT_DEFAULTS[op]
+            if op == "Selu":
+                al, be = nd.attrs.get("alpha", da), nd.attrs.get("gamma", db)
+            elif op == "HardSwish":
+                al, be = da, db
+            else:
+                al, be = nd.attrs.get("alpha", da), nd.attrs.get("beta", db)
+            layers[-1][2:5] = [op, float(np.float32(al)), float(np.float32(be))]
+            last_act = True
+        elif op in ("Sub", "Div", "Mul", "Clip", "Identity", "Flatten"):
             pass  # prologue / epilogue elementwise ops: not dense layers (onnx_ref.act evaluates them)
         else:
-            raise NotImplementedError(nd.op_type)
+            raise NotImplementedError(op)
         cur = nd.outputs[0]
     return [tuple(l) for l in layers]
 

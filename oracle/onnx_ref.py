@@ -14,8 +14,11 @@ the reference's graph uses, evaluated on the reference's own weights
   B' = B^T if transB. The shipped graph uses transB=1, alpha=beta=1
   (nodes /0/Gemm, /2/Gemm, /4/Gemm, /6/Gemm).
 * `Elu` (opset 6): y = x if x > 0 else alpha * (exp(x) - 1).
-* `Relu`, `Tanh`, `Sigmoid`, `LeakyRelu`, `MatMul`, `Add`, `Clip`, `Sub`,
-  `Div`, `Mul` for the other exported-policy graph shapes.
+* `Relu`, `Tanh`, `Sigmoid`, `LeakyRelu`, `Selu`, `Softplus`, `HardSigmoid`,
+  `HardSwish`, `Softsign`, `MatMul`, `Add`, `Clip` (opset 6 attributes or opset
+  11 inputs; NaN passes through, as onnxruntime's std::min(std::max(x, lo), hi)),
+  `Sub`, `Div`, `Mul`, `Constant` for the other exported-policy graph shapes
+  (SURVEY §8f.3), each as the ONNX operator specification states it.
 * `GRU` (opset 14), build-defined recurrent policy:
   gate order z, r, h; f = sigmoid, g = tanh;
   linear_before_reset=1:  h~ = tanh(Wh x + Wbh + r * (Rh h + Rbh))
@@ -151,7 +154,7 @@ def _tensor(buf: bytes):
 
 
 def _attr(buf: bytes):
-    name, kind, f, i, s, floats, ints = "", 0, None, None, None, [], []
+    name, kind, f, i, s, t, floats, ints = "", 0, None, None, None, None, [], []
     for fno, wt, val in _fields(buf):
         if fno == 1:
             name = val.decode()
@@ -168,12 +171,14 @@ def _attr(buf: bytes):
                 floats.append(struct.unpack("<f", val)[0])
         elif fno == 8:
             ints.extend(_signed64(v) for v in _packed_varints(val, wt))
+        elif fno == 5:                       # t: TensorProto (Constant's value)
+            t = _tensor(val)[1]
         elif fno == 20:
             kind = val
-    # AttributeProto.AttributeType: FLOAT=1 INT=2 STRING=3 FLOATS=6 INTS=7
-    value = {1: f, 2: i, 3: s, 6: floats, 7: ints}.get(kind)
+    # AttributeProto.AttributeType: FLOAT=1 INT=2 STRING=3 TENSOR=4 FLOATS=6 INTS=7
+    value = {1: f, 2: i, 3: s, 4: t, 6: floats, 7: ints}.get(kind)
     if value is None:
-        value = f if f is not None else (i if i is not None else (floats or ints or s))
+        value = f if f is not None else (i if i is not None else (t if t is not None else (floats or ints or s)))
     return name, value
 
 
@@ -386,9 +391,32 @@ def run(g: Graph, feeds: dict, dtype=np.float64) -> dict:
         elif op == "Sigmoid":
             out = {nd.outputs[0]: _sigmoid(ins[0])}
         elif op == "Clip":
-            lo = ins[1] if len(ins) > 1 and ins[1] is not None else -np.inf
-            hi = ins[2] if len(ins) > 2 and ins[2] is not None else np.inf
-            out = {nd.outputs[0]: np.clip(ins[0], lo, hi)}
+            lo = ins[1] if len(ins) > 1 and ins[1] is not None else a.get("min", -np.inf)
+            hi = ins[2] if len(ins) > 2 and ins[2] is not None else a.get("max", np.inf)
+            x = ins[0]
+            out = {nd.outputs[0]: np.where(x < lo, lo, np.where(x > hi, hi, x)).astype(dt)}
+        elif op == "Selu":
+            al, ga = dt.type(a.get("alpha", 1.67326319217681884765625)), dt.type(a.get("gamma", 1.05070102214813232421875))
+            x = ins[0]
+            out = {nd.outputs[0]: ga * np.where(x > 0, x, al * np.expm1(np.minimum(x, 0)))}
+        elif op == "Softplus":
+            x = ins[0]
+            out = {nd.outputs[0]: np.maximum(x, 0) + np.log1p(np.exp(-np.abs(x)))}
+        elif op in ("HardSigmoid", "HardSwish"):
+            if op == "HardSigmoid":
+                al, be = dt.type(a.get("alpha", 0.2)), dt.type(a.get("beta", 0.5))
+            else:
+                al, be = dt.type(1.0 / 6.0), dt.type(0.5)
+            x = ins[0]
+            hs = np.clip(al * x + be, 0, 1)
+            out = {nd.outputs[0]: hs if op == "HardSigmoid" else x * hs}
+        elif op == "Softsign":
+            out = {nd.outputs[0]: ins[0] / (1 + np.abs(ins[0]))}
+        elif op == "Constant":
+            v = a.get("value")
+            if v is None:
+                v = a.get("value_float", a.get("value_floats"))
+            out = {nd.outputs[0]: np.asarray(v, dtype=dt)}
         elif op == "GRU":
             out = _gru(nd, env, dt)
         elif op == "LSTM":

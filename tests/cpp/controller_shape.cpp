@@ -1,7 +1,10 @@
 // "Controller-shaped" use of the drop-in header, exactly as the reference's
 // callers use it (onnx_controller/src/controller.cpp:25,49,215 with the
 // std::array members of controller.hpp:148-149; onnx_inference/src/cpp/main.cpp:32-45).
-// Usage: controller_shape <model.onnx> [zeros|twos|ticks N]
+// Usage: controller_shape <model.onnx> [zeros|twos|ticks N [actions.bin]]
+//   ticks: N act() calls on an observation the caller changes in place before each
+//   (observation[t % 98] += 0.001f, as populate_buffer rewrites it every tick); with
+//   actions.bin, every tick's 12 actions are written there as float32 [N][12].
 //        controller_shape <model.onnx> lat <iters> <warmup> <in_dim> <out_dim>
 //   lat: act() latency as the reference's main.cpp:38-42 measures it (steady_clock
 //   around one act()), over <warmup> untimed then <iters> timed calls on spans of
@@ -55,6 +58,7 @@ int main(int argc, char **argv) {
     std::printf("check_dims: %d\n", actor->check_dims() ? 1 : 0);
     if (mode == "twos") observation.fill(2.0f);
     int ticks = mode == "ticks" && argc > 3 ? std::atoi(argv[3]) : 1;
+    std::FILE *dump = mode == "ticks" && argc > 4 ? std::fopen(argv[4], "wb") : nullptr;
     double best = 1e30;
     for (int t = 0; t < ticks; ++t) {
       if (mode == "ticks") observation[t % observation.size()] += 0.001f;  // obs changes every tick
@@ -62,7 +66,9 @@ int main(int argc, char **argv) {
       actor->act();
       auto t1 = std::chrono::steady_clock::now();
       best = std::min(best, std::chrono::duration<double, std::micro>(t1 - t0).count());
+      if (dump && std::fwrite(action.data(), sizeof(float), action.size(), dump) != action.size()) return 4;
     }
+    if (dump) std::fclose(dump);
     std::printf("Action:");
     for (float a : action) std::printf(" %.9g", a);
     std::printf("\nbest_us: %.3f\n", best);

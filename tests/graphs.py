@@ -1,7 +1,10 @@
 """Small ONNX policy graphs exercising the loader's supported patterns
 (SURVEY §8f.3 "ONNX loader breadth"): Gemm with transB=0 / alpha / beta,
 MatMul + Add, Sub/Div input normalisation, LeakyRelu / Sigmoid, trailing
-Tanh + Clip. Built with the repo's own writer; evaluated by the oracle."""
+Tanh + Clip, Clip between dense layers (ReLU6), Constant nodes, Mul by a
+constant at the input / after a Gemm / after an activation / at the output,
+Selu / Softplus / HardSigmoid / HardSwish / Softsign. Built with the repo's own
+writer; evaluated by the oracle."""
 import numpy as np
 
 from go2_onnx_controller_amd import onnx_writer as ow
@@ -53,10 +56,86 @@ def variant_bytes(kind: str, seed: int = 0) -> bytes:
                 nodes.append(ow.node("Relu", [cur], [f"a{i}"]))
                 cur = f"a{i}"
         return ow.model(nodes, inits, [("obs", ["N", 30])], [("act", ["N", 9])])
+    if kind == "relu6_mid_clip":
+        # Gemm -> Clip(0, 6) -> Gemm -> Elu -> Gemm: a Clip between dense layers is the
+        # first layer's activation (torch.onnx.export writes nn.ReLU6 so, opset >= 11)
+        W1, b1, W2, b2, W3, b3 = f32(64, 30) * 4, f32(64) * 4, f32(48, 64), f32(48), f32(10, 48), f32(10)
+        nodes = [ow.node("Gemm", ["obs", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Clip", ["h1", "lo", "hi"], ["a1"]),
+                 ow.node("Gemm", ["a1", "W2", "b2"], ["h2"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Elu", ["h2"], ["a2"]),
+                 ow.node("Gemm", ["a2", "W3", "b3"], ["act"], "", [ow.attr_int("transB", 1)])]
+        inits = [("W1", W1), ("b1", b1), ("lo", np.array(0, np.float32)), ("hi", np.array(6, np.float32)),
+                 ("W2", W2), ("b2", b2), ("W3", W3), ("b3", b3)]
+        return ow.model(nodes, inits, [("obs", ["N", 30])], [("act", ["N", 10])])
+    if kind == "relu6_pipeline":
+        # uniform 256-wide hidden layers with Clip(-1, 1.5) activations: the 4-wave pipeline
+        # (lean kernel, activation read at run time) with a two-parameter activation
+        dims = [40, 256, 256, 256, 12]
+        nodes, inits, cur = [], [("lo", np.array(-1.0, np.float32)), ("hi", np.array(1.5, np.float32))], "obs"
+        for i, (k, n) in enumerate(zip(dims[:-1], dims[1:])):
+            inits += [(f"W{i}", (f32(n, k) / np.sqrt(k / 12.0)).astype(np.float32)), (f"b{i}", f32(n))]
+            out = "act" if i == len(dims) - 2 else f"h{i}"
+            nodes.append(ow.node("Gemm", [cur, f"W{i}", f"b{i}"], [out], "", [ow.attr_int("transB", 1)]))
+            cur = out
+            if out != "act":
+                nodes.append(ow.node("Clip", [cur, "lo", "hi"], [f"a{i}"]))
+                cur = f"a{i}"
+        return ow.model(nodes, inits, [("obs", ["N", 40])], [("act", ["N", 12])])
+    if kind == "const_scales":
+        # scales as Constant nodes (as torch.onnx.export writes Python scalars): the observation
+        # scaled and clipped, a Mul right after a Gemm (folded into its rows), a per-feature Mul
+        # after an activation (folded into the next layer's columns), and the output clipped,
+        # then scaled (the action epilogue)
+        W1, b1, W2, b2 = f32(32, 20), f32(32), f32(8, 32), f32(8)
+        sc_in = (np.abs(f32(20)) + 0.5).astype(np.float32)
+        nodes = [ow.node("Constant", [], ["k_in"], "", [ow.attr_tensor("value", sc_in)]),
+                 ow.node("Constant", [], ["lo_in"], "", [ow.attr_tensor("value", np.array(-2.5, np.float32))]),
+                 ow.node("Constant", [], ["hi_in"], "", [ow.attr_tensor("value", np.array(2.0, np.float32))]),
+                 ow.node("Constant", [], ["k1"], "", [ow.attr_tensor("value", np.array(1.75, np.float32))]),
+                 ow.node("Constant", [], ["k2"], "", [ow.attr_tensor("value", (np.abs(f32(32)) + 0.2).astype(np.float32))]),
+                 ow.node("Constant", [], ["k_out"], "", [ow.attr_tensor("value", np.array(0.25, np.float32))]),
+                 ow.node("Mul", ["obs", "k_in"], ["x1"]),
+                 ow.node("Clip", ["x1", "lo_in", "hi_in"], ["x2"]),
+                 ow.node("Gemm", ["x2", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Mul", ["k1", "h1"], ["h1s"]),
+                 ow.node("Tanh", ["h1s"], ["a1"]),
+                 ow.node("Mul", ["a1", "k2"], ["a1s"]),
+                 ow.node("Gemm", ["a1s", "W2", "b2"], ["h2"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Elu", ["h2"], ["a2"]),
+                 ow.node("Clip", ["a2"], ["c2"], "", [ow.attr_float("min", -0.4), ow.attr_float("max", 0.9)]),
+                 ow.node("Mul", ["c2", "k_out"], ["act"])]
+        inits = [("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2)]
+        return ow.model(nodes, inits, [("obs", ["N", 20])], [("act", ["N", 8])])
+    if kind == "selu_softplus_hardswish":
+        W1, b1, W2, b2, W3, b3, W4, b4 = (f32(40, 24), f32(40), f32(40, 40), f32(40), f32(24, 40), f32(24),
+                                          f32(6, 24) * 0.25, f32(6))
+        nodes = [ow.node("Gemm", ["obs", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Selu", ["h1"], ["a1"]),
+                 ow.node("Gemm", ["a1", "W2", "b2"], ["h2"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Softplus", ["h2"], ["a2"]),
+                 ow.node("Gemm", ["a2", "W3", "b3"], ["h3"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("HardSwish", ["h3"], ["a3"]),
+                 ow.node("Gemm", ["a3", "W4", "b4"], ["h4"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("HardSigmoid", ["h4"], ["act"], "", [ow.attr_float("alpha", 0.3), ow.attr_float("beta", 0.4)])]
+        inits = [("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2), ("W3", W3), ("b3", b3), ("W4", W4), ("b4", b4)]
+        return ow.model(nodes, inits, [("obs", ["N", 24])], [("act", ["N", 6])])
+    if kind == "softsign_selu_attrs":
+        W1, b1, W2, b2 = f32(48, 16), f32(48), f32(5, 48), f32(5)
+        nodes = [ow.node("Gemm", ["obs", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Softsign", ["h1"], ["a1"]),
+                 ow.node("Gemm", ["a1", "W2", "b2"], ["h2"], "", [ow.attr_int("transB", 1)]),
+                 ow.node("Selu", ["h2"], ["act"], "", [ow.attr_float("alpha", 1.2), ow.attr_float("gamma", 0.8)])]
+        inits = [("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2)]
+        return ow.model(nodes, inits, [("obs", ["N", 16])], [("act", ["N", 5])])
     raise KeyError(kind)
 
 
-VARIANTS = ["gemm_transB0_alpha_beta", "matmul_add_sigmoid", "normalized_tanh_clip", "relu_deep"]
+VARIANTS = ["gemm_transB0_alpha_beta", "matmul_add_sigmoid", "normalized_tanh_clip", "relu_deep", "relu6_mid_clip",
+            "relu6_pipeline", "const_scales", "selu_softplus_hardswish", "softsign_selu_attrs"]
+# graphs whose every operator propagates a NaN (ONNX Clip included): a NaN observation
+# row must come out as a NaN action row
+NAN_VARIANTS = ["normalized_tanh_clip", "relu6_mid_clip", "relu6_pipeline", "const_scales"]
 
 UNSUPPORTED = {
     # op the loader must reject with a clear message (no silent fallback)
@@ -64,7 +143,43 @@ UNSUPPORTED = {
                              [("W", np.zeros((1, 1, 1), np.float32))], [("obs", [1, 4])], [("act", [1, 4])]),
     "dynamic_weight": lambda: ow.model([ow.node("MatMul", ["obs", "w_in"], ["act"])], [],
                                        [("obs", [1, 4]), ("w_in", [4, 4])], [("act", [1, 4])]),
+    # a Clip after an activation between two dense layers (not an activation of its own:
+    # the matcher fuses one activation per layer) must be refused, never moved to the output
+    "clip_after_act_mid": lambda: _chain([("Relu",), ("Clip", 0.0, 6.0)]),
+    # Mul after the last activation, then Clip: clip(s * y) is not post_fn's clip-then-scale
+    "mul_then_clip_out": lambda: _chain([], tail=[("Tanh",), ("Mul", np.float32(2.0)), ("Clip", -1.0, 1.0)]),
+    "vector_mul_out": lambda: _chain([], tail=[("Tanh",), ("Mul", np.arange(1, 5, dtype=np.float32))]),
 }
+
+
+def _chain(mid_ops, tail=()):
+    """obs[4] -> Gemm -> mid_ops -> Gemm -> tail ops -> act[4] (for the refusal cases)."""
+    r = _rng(5)
+    inits = [("W0", r.standard_normal((4, 4)).astype(np.float32)), ("W1", r.standard_normal((4, 4)).astype(np.float32))]
+    nodes, cur, k = [ow.node("Gemm", ["obs", "W0"], ["g0"], "", [ow.attr_int("transB", 1)])], "g0", 0
+
+    def apply(op):
+        nonlocal cur, k
+        k += 1
+        out = f"t{k}"
+        if op[0] == "Clip":
+            inits.extend([(f"lo{k}", np.array(op[1], np.float32)), (f"hi{k}", np.array(op[2], np.float32))])
+            nodes.append(ow.node("Clip", [cur, f"lo{k}", f"hi{k}"], [out]))
+        elif op[0] == "Mul":
+            inits.append((f"m{k}", np.asarray(op[1], np.float32)))
+            nodes.append(ow.node("Mul", [cur, f"m{k}"], [out]))
+        else:
+            nodes.append(ow.node(op[0], [cur], [out]))
+        cur = out
+
+    for op in mid_ops:
+        apply(op)
+    nodes.append(ow.node("Gemm", [cur, "W1"], ["g1"], "", [ow.attr_int("transB", 1)]))
+    cur = "g1"
+    for op in tail:
+        apply(op)
+    nodes.append(ow.node("Identity", [cur], ["act"]))
+    return ow.model(nodes, inits, [("obs", ["N", 4])], [("act", ["N", 4])])
 
 
 def write(tmp_path, kind, seed=0):

@@ -53,15 +53,17 @@ def _oracle_layers(path):
     return mlp_ref.mlp_layers(onnx_ref.load(path))
 
 
-ACT_CODE = {"none": 0, "Elu": 1, "Relu": 2, "Tanh": 3, "Sigmoid": 4, "LeakyRelu": 5}
+ACT_CODE = {"none": 0, "Elu": 1, "Relu": 2, "Tanh": 3, "Sigmoid": 4, "LeakyRelu": 5, "Clip": 6, "Selu": 7,
+            "Softplus": 8, "HardSigmoid": 9, "HardSwish": 10, "Softsign": 11}
 
 
 def _check_layers(view, layers):
     assert len(view["layers"]) == len(layers)
-    for v, (W, b, act, alpha) in zip(view["layers"], layers):
+    for v, (W, b, act, alpha, beta) in zip(view["layers"], layers):
         assert (v["N"], v["K"]) == W.shape
         assert v["act"] == ACT_CODE[act]
         assert v["alpha"] == pytest.approx(alpha, abs=1e-7)
+        assert v["beta"] == pytest.approx(beta, abs=1e-7)
         assert v["w_sum"] == pytest.approx(float(W.astype(np.float64).sum()), rel=1e-9, abs=1e-9)
         assert v["b_sum"] == pytest.approx(float(b.astype(np.float64).sum()), rel=1e-9, abs=1e-9)
 
@@ -109,10 +111,19 @@ def test_loader_graph_variants(tmp_path, kind):
     if kind == "normalized_tanh_clip":
         assert v["pre_sub"] == 24 and v["pre_div"] == 24
         assert v["clip"] == pytest.approx([-0.5, 0.75])
+    if kind == "relu6_mid_clip":  # the Clip is layer 0's activation, not an output clip
+        assert v["clip"] == [-1e308, 1e308] and v["layers"][0]["act"] == 6
+        assert (v["layers"][0]["alpha"], v["layers"][0]["beta"]) == (0.0, 6.0)
+    if kind == "const_scales":
+        assert v["pre_mul"] == 20 and v["pre_clip"] == pytest.approx([-2.5, 2.0])
+        assert v["clip"] == pytest.approx([-0.4, 0.9]) and v["post_scale"] == 0.25
 
 
 @pytest.mark.parametrize("kind,msg", [("conv", "unsupported operator 'Conv'"),
-                                      ("dynamic_weight", "not an initializer")])
+                                      ("dynamic_weight", "not an initializer"),
+                                      ("clip_after_act_mid", "only supported at the end of the graph"),
+                                      ("mul_then_clip_out", "Clip after a Mul"),
+                                      ("vector_mul_out", "per-feature Mul after the final activation")])
 def test_loader_rejects_unsupported(tmp_path, kind, msg):
     from go2_onnx_controller_amd import engine
     with pytest.raises(engine.Go2piError, match=msg):
@@ -260,3 +271,32 @@ def test_loader_rejects_unsupported_lstm_forms(synth_path):
             fh.flush()
             with pytest.raises(Go2piError, match=msg):
                 inspect_model(fh.name)
+
+
+def test_loader_state_io_traced_by_name(tmp_path):
+    """An LSTM policy whose graph lists its state I/O as (c, h): the loader maps them
+    to the cell's initial_h / initial_c and Y_h / Y_c by name and lists them (h, c),
+    the engine's state-row order (they were taken by position)."""
+    from go2_onnx_controller_amd import onnx_writer as ow
+    from go2_onnx_controller_amd.engine import inspect_model
+    H, I = 16, 6
+    rng = np.random.default_rng(0)
+    inits = [("lstm.W", rng.standard_normal((1, 4 * H, I)).astype(np.float32)),
+             ("lstm.R", rng.standard_normal((1, 4 * H, H)).astype(np.float32)),
+             ("axes0", np.array([0], np.int64)), ("w", rng.standard_normal((3, H)).astype(np.float32))]
+    nodes = [ow.node("Unsqueeze", ["observation", "axes0"], ["x_seq"], "u"),
+             ow.node("Identity", ["cc_in"], ["c0"], "ic"),
+             ow.node("LSTM", ["x_seq", "lstm.W", "lstm.R", "", "", "hh_in", "c0"], ["Y", "h_o", "c_o"], "lstm",
+                     [ow.attr_int("hidden_size", H)]),
+             ow.node("Identity", ["c_o"], ["cc_out"], "oc"),
+             ow.node("Squeeze", ["h_o", "axes0"], ["h"], "s"),
+             ow.node("Identity", ["h_o"], ["hh_out"], "oh"),
+             ow.node("Gemm", ["h", "w"], ["action"], "g", [ow.attr_int("transB", 1)])]
+    data = ow.model(nodes, inits, [("observation", ["batch", I]), ("cc_in", [1, "batch", H]),
+                                   ("hh_in", [1, "batch", H])],
+                    [("action", ["batch", 3]), ("cc_out", [1, "batch", H]), ("hh_out", [1, "batch", H])])
+    p = tmp_path / "lstm_ch.onnx"
+    p.write_bytes(data)
+    v = inspect_model(str(p))
+    assert [i["name"] for i in v["inputs"]] == ["observation", "hh_in", "cc_in"]
+    assert [o["name"] for o in v["outputs"]] == ["action", "hh_out", "cc_out"]

@@ -37,12 +37,25 @@ def test_cpp_onnx_actor_known_answers(mode, resident):
 
 
 @pytest.mark.parametrize("resident", ["100", "0"])
-def test_cpp_onnx_actor_ticks(resident):
+def test_cpp_onnx_actor_ticks(resident, tmp_path):
+    """500 ticks of the C++ shim with the observation rewritten in place before each
+    act() (controller.cpp:200-215 at 50 Hz): every tick's action against the fp64
+    oracle on the same observation sequence, in the resident and launch-per-call forms."""
+    from oracle import mlp_ref
     exe = build_controller_shape()
-    r = subprocess.run([exe, SHIPPED, "ticks", "500"], capture_output=True, text=True, timeout=120,
+    dump, ticks = tmp_path / "actions.bin", 500
+    r = subprocess.run([exe, SHIPPED, "ticks", str(ticks), str(dump)], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, GO2PI_RESIDENT_MS=resident))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "best_us:" in r.stdout
+    got = np.fromfile(dump, np.float32).reshape(ticks, 12)
+    obs, seq = np.zeros(98, np.float32), np.empty((ticks, 98), np.float32)
+    for t in range(ticks):  # the same float32 in-place updates as the C++ loop
+        obs[t % 98] += np.float32(0.001)
+        seq[t] = obs
+    want = mlp_ref.MlpRef.from_onnx(SHIPPED).f64(seq)
+    assert abs_err(got, want) <= TOL
+    assert len(np.unique(got[:, 0])) > ticks // 2  # the actions follow the changing observation
 
 
 def test_python_onnx_actor_aliasing(capsys):
@@ -75,9 +88,14 @@ def test_inference_session_mirror():
     assert rel_err(y, want) <= TOL
 
 
+# (batch, resident_ms): batch <= 8 runs the single-launch latency kernel (0) or the
+# resident kernel (100); 300 the batched kernel (the 4-wave pipeline where it applies)
+PATHS = [(1, 0), (1, 100), (5, 0), (5, 100), (300, 0)]
+
+
 @pytest.mark.parametrize("kind", graphs.VARIANTS)
-@pytest.mark.parametrize("B", [1, 5, 300])
-def test_graph_variants_on_gpu(tmp_path, kind, B):
+@pytest.mark.parametrize("B,res", PATHS)
+def test_graph_variants_on_gpu(tmp_path, kind, B, res):
     from go2_onnx_controller_amd import Engine
     from oracle import onnx_ref
     p = graphs.write(tmp_path, kind, seed=B)
@@ -89,10 +107,37 @@ def test_graph_variants_on_gpu(tmp_path, kind, B):
     # path (oracle in float32) is 4.9e-5 off element-wise. The fp32 rounding scale
     # is the activations' magnitude, so the bound is normwise:
     # max|y - ref| / max(1, max|ref|) <= 1e-5.
-    with Engine(p, max_batch=512) as e:
+    with Engine(p, max_batch=512, resident_ms=res) as e:
         y = e.run(x)
+        y2 = e.run(x)  # a second call (the resident kernel: the live one answers)
     assert abs_err(y, want) / max(1.0, float(np.abs(want).max())) <= TOL
+    np.testing.assert_array_equal(y2, y)
     assert abs_err(onnx_ref.act(g, x, dtype=np.float32), want) / max(1.0, float(np.abs(want).max())) <= TOL
+
+
+@pytest.mark.parametrize("kind", graphs.NAN_VARIANTS)
+@pytest.mark.parametrize("B,res", PATHS)
+def test_graph_nan_propagates(tmp_path, kind, B, res):
+    """ONNX Clip / Elu / Tanh propagate a NaN (onnxruntime's Clip is
+    std::min(std::max(x, lo), hi)): a NaN in an observation row makes that row's
+    actions NaN on every kernel path, never the clip bound, and leaves the other
+    rows untouched."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    p = graphs.write(tmp_path, kind, seed=B)
+    g = onnx_ref.load(p)
+    x = np.random.default_rng(B).standard_normal((B, g.inputs[0][1][1])).astype(np.float32)
+    x[0, 3] = np.nan
+    if B > 2:
+        x[B - 1, 0] = np.nan
+    want = onnx_ref.act(g, x.astype(np.float64))
+    assert np.isnan(want[0]).all()
+    with Engine(p, max_batch=512, resident_ms=res) as e:
+        y = e.run(x)
+    np.testing.assert_array_equal(np.isnan(y), np.isnan(want))
+    ok = ~np.isnan(want)
+    if ok.any():
+        assert abs_err(y[ok], want[ok]) / max(1.0, float(np.abs(want[ok]).max())) <= TOL
 
 
 def _free_port():
@@ -116,3 +161,40 @@ def test_fleet_two_ranks_bitwise(tmp_path, synth_path):
         want = e.run(obs)
     for r in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"rank{r}.npy"), want)
+
+
+def test_configs3_fleet_at_size(synth_path):
+    """BASELINE configs[3] at its size on the HIP path: 32,768 robots of the
+    48->512^3->12 policy, seed-1 observations. The full batch in
+    one launch is bitwise equal to the eight contiguous 4,096-row shards
+    fleet.shard_range gives the eight ranks (each robot's row runs the same
+    instruction sequence wherever it sits), and 256 sampled rows —
+    the first and last 16-row tile of every shard among them — are within 1e-5 of
+    the fp64 oracle."""
+    import torch
+    from go2_onnx_controller_amd import Engine, fleet
+    from oracle import mlp_ref
+    B, world, path = 32768, 8, synth_path("go2_mlp_512")
+    obs = np.random.default_rng(1).standard_normal((B, 48)).astype(np.float32)
+    x = torch.from_numpy(obs).to("cuda:0")
+    with Engine(path, max_batch=B) as e:
+        full = e.run_torch(x)
+        shards = torch.empty_like(full)
+        for r in range(world):
+            a, b = fleet.shard_range(B, r, world)
+            assert b - a == 4096
+            e.run_torch(x[a:b], out=shards[a:b])
+        torch.cuda.synchronize()
+    full, shards = full.cpu().numpy(), shards.cpu().numpy()
+    np.testing.assert_array_equal(full, shards)
+    rows = set()
+    for r in range(world):
+        a, b = fleet.shard_range(B, r, world)
+        rows.update(range(a, a + 16))
+        rows.update(range(b - 16, b))
+    rng = np.random.default_rng(3)
+    while len(rows) < 256:
+        rows.add(int(rng.integers(0, B)))
+    rows = np.array(sorted(rows))
+    ref = mlp_ref.MlpRef.from_onnx(path).f64(obs[rows])
+    assert abs_err(full[rows], ref) <= TOL

@@ -406,3 +406,52 @@ def test_batched_launch_evicts_other_resident_kernels(synth_path):
             th.join(timeout=10)
     assert not errs, errs
     assert n_act[0] > 10
+
+
+@pytest.mark.parametrize("name", ["gru_128", "lstm_128"])
+def test_batched_launch_evicts_recurrent_resident_kernel(synth_path, name):
+    """The eviction race of ADVICE r03 on a recurrent policy: while another engine's
+    4096-robot launches keep evicting it, the resident GRU / LSTM engine's act() runs
+    a rollout from another thread. A request the kernel answered just before it left
+    must not be served a second time (that would step the hidden state twice), so
+    every action and the final hidden rows match the fp64 oracle rollout."""
+    import threading
+    import torch
+    from go2_onnx_controller_amd import Engine
+    p, pb = synth_path(name), synth_path("go2_mlp_512")
+    step = _lstm_oracle_step if name.startswith("lstm") else _gru_oracle_step
+    rng = np.random.default_rng(41)
+    xs = [rng.standard_normal((1 + i % 2, 30)).astype(np.float32) for i in range(60)]
+    errs, got = [], []
+    stop = threading.Event()
+    with Engine(p, max_batch=8, resident_ms=1000) as a, Engine(pb, max_batch=4096) as b:
+        a.reset_hidden()
+
+        def tick():
+            try:
+                for x in xs:
+                    got.append(a.run(x).copy())
+                    time.sleep(0.0005)
+            except Exception as ex:  # noqa: BLE001 - reported below
+                errs.append(repr(ex))
+            finally:
+                stop.set()
+        th = threading.Thread(target=tick)
+        th.start()
+        xb = torch.randn((4096, 48), device="cuda:0")
+        s = torch.cuda.Stream()
+        n = 0
+        while not stop.is_set() and n < 2000:
+            b.run_torch(xb, stream=s)
+            s.synchronize()
+            n += 1
+        th.join(timeout=30)
+        assert not errs, errs
+        assert len(got) == len(xs) and n > 5
+        h_ref = np.zeros((8, a.hidden_dim))
+        for i, x in enumerate(xs):
+            B = x.shape[0]
+            want, h_new = step(p, x, h_ref[:B])
+            h_ref[:B] = h_new
+            assert abs_err(got[i], want) <= TOL, f"request {i}"
+        assert abs_err(a.get_hidden(8), h_ref) <= TOL
