@@ -126,6 +126,9 @@ def cpu_baseline(model_path, in_dim, batch, seconds=8.0):
                       f"(oracle/mlp_ref.c, -O3 x86-64-v3, OpenMP {nthr} threads) on {cpu_model_name()}",
             "single_thread": {"value": v1, "cores": 1, "sample": f"{n1} steps x {batch} robots ({e1:.1f} s)"},
             "cpu_model": cpu_model_name(), "host_cpus_allowed": allowed,
+            "threads_leg": (f"{nthr} threads: OMP_NUM_THREADS, the GPU box's CPU share per GPU (host_cpus_allowed "
+                            f"counts the whole machine's {allowed}, shared with other jobs)") if nthr != allowed
+                           else f"{nthr} threads: every CPU this process may run on",
             "configs0_batch1": dict(b1, warmup=1000, iters=10000, threads=1,
                                     what="one single-robot fp32 forward per call, timed in C "
                                          "(the reference's main.cpp:38-42 measurement)")}

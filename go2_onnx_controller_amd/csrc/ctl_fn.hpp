@@ -91,7 +91,8 @@ struct CtlLds {
 
 __host__ __device__ inline int ctl_lds_floats(int R, int in_dim) {
   auto c64 = [](int x) { return (x + 63) & ~63; };
-  return 24 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) + c64(R * in_dim) +
+  // q0: 12 doubles, copied by one direct-to-LDS instruction (64 lanes x 4 B: 64 floats of room)
+  return 64 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) + c64(R * in_dim) +
          GO2PI_TILE_ROWS;
 }
 
@@ -99,7 +100,7 @@ __device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim) {
   auto c64 = [](int x) { return (x + 63) & ~63; };
   CtlLds L;
   L.q0 = reinterpret_cast<double *>(base);
-  L.st = base + 24;
+  L.st = base + 64;
   L.jy = L.st + c64(R * GO2PI_CTL_STATE_DIM);
   L.act = L.jy + c64(R * GO2PI_CTL_JOY_DIM);
   L.obs = L.act + c64(R * GO2PI_CTL_DOF);
@@ -107,14 +108,17 @@ __device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim) {
   return L;
 }
 
-// Issue the direct-to-LDS loads of rows [row0, row0 + nrows) and clear the NaN flags.
+// Issue the direct-to-LDS loads of rows [row0, row0 + nrows) and of q0, and clear
+// the NaN flags. Nothing here waits for memory: the loads land by the issuing
+// waves' next vmcnt wait (lds_dma_wait, or the pipeline's wg_barrier_vm).
 __device__ __forceinline__ void ctl_lds_load(const CtlLds L, const DevCtl C, int row0, int nrows, int in_dim, int tid,
                                              int wave, int lane, int nw) {
+  glds_copy(reinterpret_cast<float *>(L.q0), reinterpret_cast<const float *>(C.prm->q0), 2 * GO2PI_CTL_DOF, wave, lane,
+            nw);
   glds_copy(L.st, C.state + (size_t)row0 * GO2PI_CTL_STATE_DIM, nrows * GO2PI_CTL_STATE_DIM, wave, lane, nw);
   if (C.joy) glds_copy(L.jy, C.joy + (size_t)row0 * GO2PI_CTL_JOY_DIM, nrows * GO2PI_CTL_JOY_DIM, wave, lane, nw);
   glds_copy(L.act, C.action + (size_t)row0 * GO2PI_CTL_DOF, nrows * GO2PI_CTL_DOF, wave, lane, nw);
   glds_copy(L.obs, C.obs + (size_t)row0 * in_dim, nrows * in_dim, wave, lane, nw);
-  if (tid < GO2PI_CTL_DOF) L.q0[tid] = C.prm->q0[tid];
   if (tid < GO2PI_TILE_ROWS) L.nanf[tid] = 0u;
 }
 

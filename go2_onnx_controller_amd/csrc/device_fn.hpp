@@ -22,23 +22,45 @@ __device__ __forceinline__ float sigmoid_fast(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
+// ONNX Softplus ln(exp(x) + 1) in the overflow-free form max(x, 0) + ln(1 + exp(-|x|))
+// on v_exp_f32 / v_log_f32 (~1 ulp each): the 1 + t rounding costs at most half an
+// ulp of 1 (4e-8 absolute after the ln 2 scale); a NaN propagates through the log.
+__device__ __forceinline__ float softplus_fast(float x) {
+  const float t = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+  return fmaxf(x, 0.f) + __builtin_amdgcn_logf(1.f + t) * 0.6931471805599453f;
+}
+
 // ONNX Clip (opset 11+): std::min(std::max(x, lo), hi) as onnxruntime computes it,
 // so a NaN passes through (fminf / fmaxf would return the bound instead).
 __device__ __forceinline__ float clip_nan(float x, float lo, float hi) {
   return x < lo ? lo : (x > hi ? hi : x);
 }
 
+// A dense layer's activation and its ONNX attributes (Elu / LeakyRelu alpha; Clip
+// min / max; Selu alpha / gamma; HardSigmoid alpha / beta), Act in onnx_model.hpp.
+struct ActP {
+  int act;
+  float alpha, beta;
+};
+
+// the kind of every activation after the six of r01-r03 (Clip, Selu, Softplus,
+// HardSigmoid, HardSwish, Softsign) as one compile-time case: its epilogue applies
+// act_fn per element (a branch on the uniform kind), which keeps the number of
+// epilogue instantiations of every kernel template at seven
+#define GO2PI_ACT_RT 100
+
+__device__ __forceinline__ float act_fn(int act, float alpha, float beta, float x);
+
 // Activation with the kind known at compile time: epilogues dispatch ONCE per
 // tile group (a runtime switch per element made hipcc emit every activation's
 // code, an IEEE divide and a vmcnt(0) wait for each of the 16 elements per lane:
-// measured 4.4K cycles per layer epilogue). alpha / beta: the node's attributes
-// (Elu / LeakyRelu alpha; Clip min / max; Selu alpha / gamma; HardSigmoid alpha /
-// beta), Act in onnx_model.hpp.
+// measured 4.4K cycles per layer epilogue).
 template <int ACT>
-__device__ __forceinline__ float act_t(float alpha, float beta, float x) {
+__device__ __forceinline__ float act_t(const ActP &a, float x) {
 #ifdef GO2PI_DIAG_NOEPI
   return x;
 #endif
+  const float alpha = a.alpha, beta = a.beta;
   if constexpr (ACT == 1) return x > 0.f ? x : alpha * expm1_neg(x);  // Elu (ONNX opset 6)
   else if constexpr (ACT == 2) return x > 0.f ? x : 0.f;              // Relu
   else if constexpr (ACT == 3) return tanhf(x);                       // Tanh
@@ -46,48 +68,44 @@ __device__ __forceinline__ float act_t(float alpha, float beta, float x) {
   else if constexpr (ACT == 5) return x >= 0.f ? x : alpha * x;       // LeakyRelu
   else if constexpr (ACT == 6) return clip_nan(x, alpha, beta);       // Clip (ReLU6: 0, 6)
   else if constexpr (ACT == 7) return x > 0.f ? beta * x : beta * (alpha * expm1_neg(x));  // Selu
-  else if constexpr (ACT == 8) return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));             // Softplus
+  else if constexpr (ACT == 8) return softplus_fast(x);                                     // Softplus
   else if constexpr (ACT == 9) return clip_nan(alpha * x + beta, 0.f, 1.f);                // HardSigmoid
   else if constexpr (ACT == 10) return x * clip_nan(alpha * x + beta, 0.f, 1.f);           // HardSwish
-  else if constexpr (ACT == 11) return x / (1.f + fabsf(x));                               // Softsign
+  else if constexpr (ACT == 11) return x * __builtin_amdgcn_rcpf(1.f + fabsf(x));          // Softsign (rcp: ~1 ulp)
+  else if constexpr (ACT == GO2PI_ACT_RT) return act_fn(a.act, alpha, beta, x);
   else return x;
 }
 
-#define GO2PI_NUM_ACTS 12
-
 __device__ __forceinline__ float act_fn(int act, float alpha, float beta, float x) {
+  const ActP a{act, alpha, beta};
   switch (act) {
-    case 1: return act_t<1>(alpha, beta, x);
-    case 2: return act_t<2>(alpha, beta, x);
-    case 3: return act_t<3>(alpha, beta, x);
-    case 4: return act_t<4>(alpha, beta, x);
-    case 5: return act_t<5>(alpha, beta, x);
-    case 6: return act_t<6>(alpha, beta, x);
-    case 7: return act_t<7>(alpha, beta, x);
-    case 8: return act_t<8>(alpha, beta, x);
-    case 9: return act_t<9>(alpha, beta, x);
-    case 10: return act_t<10>(alpha, beta, x);
-    case 11: return act_t<11>(alpha, beta, x);
-    default: return act_t<0>(alpha, beta, x);
+    case 1: return act_t<1>(a, x);
+    case 2: return act_t<2>(a, x);
+    case 3: return act_t<3>(a, x);
+    case 4: return act_t<4>(a, x);
+    case 5: return act_t<5>(a, x);
+    case 6: return act_t<6>(a, x);
+    case 7: return act_t<7>(a, x);
+    case 8: return act_t<8>(a, x);
+    case 9: return act_t<9>(a, x);
+    case 10: return act_t<10>(a, x);
+    case 11: return act_t<11>(a, x);
+    default: return x;
   }
 }
 
-// Calls f(std::integral_constant<int, ACT>) for the runtime activation kind.
+// Calls f(std::integral_constant<int, ACT>) for the runtime activation kind (the
+// kinds past LeakyRelu share GO2PI_ACT_RT).
 template <class F>
 __device__ __forceinline__ void with_act(int act, F &&f) {
   switch (act) {
+    case 0: f(std::integral_constant<int, 0>{}); break;
     case 1: f(std::integral_constant<int, 1>{}); break;
     case 2: f(std::integral_constant<int, 2>{}); break;
     case 3: f(std::integral_constant<int, 3>{}); break;
     case 4: f(std::integral_constant<int, 4>{}); break;
     case 5: f(std::integral_constant<int, 5>{}); break;
-    case 6: f(std::integral_constant<int, 6>{}); break;
-    case 7: f(std::integral_constant<int, 7>{}); break;
-    case 8: f(std::integral_constant<int, 8>{}); break;
-    case 9: f(std::integral_constant<int, 9>{}); break;
-    case 10: f(std::integral_constant<int, 10>{}); break;
-    case 11: f(std::integral_constant<int, 11>{}); break;
-    default: f(std::integral_constant<int, 0>{}); break;
+    default: f(std::integral_constant<int, GO2PI_ACT_RT>{}); break;
   }
 }
 

@@ -148,6 +148,7 @@ struct go2pi_engine {
   bool resident_ctl_ok = false;  // the controller-tick form applies (dense policies)
   unsigned long long *d_hgran = nullptr;  // GRU form: [2][SMALL_MAXB][H] hidden-row granules (two buffers)
   bool resident_ctl = false;  // the live kernel is the controller-tick form
+  bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
   unsigned long long *d_mirror = nullptr;                 // device copy of the request (workgroup 0 -> the rest)
@@ -267,9 +268,13 @@ struct go2pi_engine {
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     std::memset(h_actg, 0, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)model.out_dim);
-    hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,
-                                     res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
-              "resident launch");
+    if (!ctl && resident1)
+      hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, stream),
+                "resident launch (one workgroup)");
+    else
+      hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,
+                                       res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
+                "resident launch");
     resident_live = true;
     res_flag.store(1);
     resident_ctl = ctl != nullptr;
@@ -861,6 +866,10 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
     if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
   }
+  // a dense policy whose weights fit one CU's registers is served by the single-
+  // workgroup resident kernel (no inter-workgroup hop per layer; GO2PI_RES_MULTI=1:
+  // the multi-workgroup form, A/B diagnostics)
+  e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p) && !std::getenv("GO2PI_RES_MULTI");
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
@@ -1379,49 +1388,7 @@ int go2pi_inspect_model(const char *path, char *buf, size_t cap) {
     } catch (const std::exception &ex) {
       throw ApiError(ex.what(), GO2PI_E_MODEL);
     }
-    auto num = [](double v) {
-      if (std::isinf(v)) return std::string(v > 0 ? "1e308" : "-1e308");
-      char t[64];
-      std::snprintf(t, sizeof t, "%.17g", v);
-      return std::string(t);
-    };
-    auto sum = [](const std::vector<float> &v) {
-      double s = 0;
-      for (float x : v) s += x;
-      return s;
-    };
-    auto io = [&](const std::vector<go2pi::IoInfo> &v) {
-      std::string s = "[";
-      for (size_t i = 0; i < v.size(); ++i) {
-        s += (i ? "," : "") + std::string("{\"name\":\"") + v[i].name + "\",\"shape\":[";
-        for (size_t d = 0; d < v[i].shape.size(); ++d) s += (d ? "," : "") + std::to_string(v[i].shape[d]);
-        s += "]}";
-      }
-      return s + "]";
-    };
-    std::string j = "{\"ir_version\":" + std::to_string(m.ir_version) + ",\"opset\":" + std::to_string(m.opset) +
-                    ",\"producer\":\"" + m.producer + "\",\"inputs\":" + io(m.inputs) + ",\"outputs\":" +
-                    io(m.outputs) + ",\"in_dim\":" + std::to_string(m.in_dim) +
-                    ",\"out_dim\":" + std::to_string(m.out_dim) + ",\"layers\":[";
-    for (size_t l = 0; l < m.layers.size(); ++l) {
-      const auto &d = m.layers[l];
-      j += (l ? "," : "") + std::string("{\"K\":") + std::to_string(d.K) + ",\"N\":" + std::to_string(d.N) +
-           ",\"act\":" + std::to_string(d.act) + ",\"alpha\":" + num(d.alpha) + ",\"beta\":" + num(d.beta) +
-           ",\"w_sum\":" + num(sum(d.W)) +
-           ",\"b_sum\":" + num(sum(d.b)) + "}";
-    }
-    j += "],\"gru\":";
-    if (m.has_gru)
-      j += "{\"cell\":\"" + std::string(m.gru.cell ? "LSTM" : "GRU") + "\",\"I\":" + std::to_string(m.gru.I) +
-           ",\"H\":" + std::to_string(m.gru.H) + ",\"lbr\":" +
-           std::to_string(m.gru.lbr) + ",\"w_sum\":" + num(sum(m.gru.W)) + ",\"r_sum\":" + num(sum(m.gru.R)) +
-           ",\"b_sum\":" + num(sum(m.gru.Wb) + sum(m.gru.Rb)) + "}";
-    else
-      j += "null";
-    j += ",\"pre_sub\":" + std::to_string(m.pre_sub.size()) + ",\"pre_div\":" + std::to_string(m.pre_div.size()) +
-         ",\"pre_mul\":" + std::to_string(m.pre_mul.size()) + ",\"pre_clip\":[" + num(m.pre_lo) + "," +
-         num(m.pre_hi) + "],\"clip\":[" + num(m.clip_lo) + "," + num(m.clip_hi) + "],\"post_scale\":" +
-         num(m.post_scale) + "}";
+    const std::string j = go2pi::inspect_json(m);
     const size_t k = std::min(cap - 1, j.size());
     std::memcpy(buf, j.data(), k);
     buf[k] = 0;

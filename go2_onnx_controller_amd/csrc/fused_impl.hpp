@@ -259,16 +259,16 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
   const int rob = lane & 15, n0 = (lane >> 4) << 2;
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
-    const float alpha = L.alpha, beta = L.beta;
+    const ActP ap{L.act, L.alpha, L.beta};
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int t = t_first + i;
       if (t >= T) continue;
       float4 v;
-      v.x = act_t<ACT>(alpha, beta, acc[i][0] + bv[i].x);
-      v.y = act_t<ACT>(alpha, beta, acc[i][1] + bv[i].y);
-      v.z = act_t<ACT>(alpha, beta, acc[i][2] + bv[i].z);
-      v.w = act_t<ACT>(alpha, beta, acc[i][3] + bv[i].w);
+      v.x = act_t<ACT>(ap, acc[i][0] + bv[i].x);
+      v.y = act_t<ACT>(ap, acc[i][1] + bv[i].y);
+      v.z = act_t<ACT>(ap, acc[i][2] + bv[i].z);
+      v.w = act_t<ACT>(ap, acc[i][3] + bv[i].w);
       if (!last) {
         *reinterpret_cast<float4 *>(Y + rob * ys + t * 16 + n0) = v;
         if constexpr (KEEP) keep[i] = v;
@@ -683,12 +683,12 @@ __device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW],
 
 // bias + activation of one 16 x 16 tile (output-major: one float4 per lane)
 template <int ACT>
-__device__ __forceinline__ float4 w4_epi(float alpha, float beta, const f32x4 &acc, const float4 &bv) {
+__device__ __forceinline__ float4 w4_epi(const ActP &ap, const f32x4 &acc, const float4 &bv) {
   float4 v;
-  v.x = act_t<ACT>(alpha, beta, acc[0] + bv.x);
-  v.y = act_t<ACT>(alpha, beta, acc[1] + bv.y);
-  v.z = act_t<ACT>(alpha, beta, acc[2] + bv.z);
-  v.w = act_t<ACT>(alpha, beta, acc[3] + bv.w);
+  v.x = act_t<ACT>(ap, acc[0] + bv.x);
+  v.y = act_t<ACT>(ap, acc[1] + bv.y);
+  v.z = act_t<ACT>(ap, acc[2] + bv.z);
+  v.w = act_t<ACT>(ap, acc[3] + bv.w);
   return v;
 }
 
@@ -1177,9 +1177,24 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     hot.head_beta = P.head_beta;
   }
   GO2PI_STAMP(P, threadIdx.x == 0 && step == 0, 42);
+  bool ctl_here = false;
+  if constexpr (CTL) {
+    // controller tick without a recurrent cell (fused_body ctl_late): the tick's raw rows
+    // (direct-to-LDS, issued at kernel start) and the biases land behind the ring's
+    // loads, which stay in flight; then the observation is assembled into X0 and
+    // published to the caller's rows, and an LDS-only barrier hands X0 over
+    ctl_here = step == 0 && !P.has_gru;
+    if (ctl_here) {
+      wg_barrier_vm<RD * TPW>();
+      GO2PI_STAMP(P, threadIdx.x == 0, 5);
+      ctl_assemble_flat<true>(P, CL, ctl_q(ctl), ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
+                              ctl.obs + (size_t)row0 * P.in_dim, threadIdx.x, 256);
+      lds_barrier();
+    }
+  }
   // layer 0's input rows are complete in X0 and the biases in LDS (this wave's
   // direct-to-LDS loads, older than the ring's); the ring's loads stay in flight
-  wg_barrier_vm<RD * TPW>();
+  if (!ctl_here) wg_barrier_vm<RD * TPW>();
   GO2PI_STAMP(P, threadIdx.x == 0 && step == 0, 4);
   if constexpr (CTL) {
     if (ctl.status && (int)threadIdx.x < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + threadIdx.x] = CL.nanf[threadIdx.x];
@@ -1218,7 +1233,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   GO2PI_STAMP(P, lane == 0 && step == 0, 16 + 3 * wave);
   GO2PI_STAMP(P, lane == 0 && step == 0 && wave == 0, 6);
   float *Y = Y0;  // where the previous layer's activations go
-  const float alpha = hot.hid_alpha, beta = hot.hid_beta;
+  const ActP ap{hot.hid_act, hot.hid_alpha, hot.hid_beta};
 #pragma unroll(NHC > 0 ? NHC : 1)
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
@@ -1249,7 +1264,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if constexpr (ACTC == 1) v[i] = w4_epi_elu1<BIN>(acc[i], bv[i]);
-        else v[i] = w4_epi<ACT>(alpha, beta, acc[i], bv[i]);
+        else v[i] = w4_epi<ACT>(ap, acc[i], bv[i]);
       }
 #pragma unroll
       for (int i = 0; i < TPW; ++i) *reinterpret_cast<float4 *>(yrow + i * 16) = v[i];
@@ -1314,7 +1329,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       for (int i = 0; i < TPW; ++i) {
         float4 v;
         if constexpr (ACTC == 1) v = w4_epi_elu1<BIN>(acc[i], bv[i]);
-        else v = w4_epi<ACT>(alpha, beta, acc[i], bv[i]);
+        else v = w4_epi<ACT>(ap, acc[i], bv[i]);
 #pragma unroll
         for (int h = 0; h < HT; ++h) {
 #pragma unroll
@@ -1345,7 +1360,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
       with_act(hot.head_act, [&](auto act_k) {
         constexpr int ACT = decltype(act_k)::value;
-        const float4 v = w4_epi<ACT>(hot.head_alpha, hot.head_beta, hs[0], hbv[0]);
+        const float4 v = w4_epi<ACT>(ActP{hot.head_act, hot.head_alpha, hot.head_beta}, hs[0], hbv[0]);
         if (row < B) {  // (lean kernel: ac = the action rows of all steps, this step's at step * B
                         // rows; general body: ac = this step's rows already)
           float *o = ac + ((PL ? (size_t)step * B : (size_t)0) + row) * hot.head_n;
@@ -1472,19 +1487,26 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const CtlLds CL = ctl_lds(lbias + P.w4_bias, GO2PI_TILE_ROWS, P.in_dim);
   CtlView cv{};
   CtlQ cq{};
+  // the pipeline without a recurrent cell assembles the tick's observation inside
+  // w4_step, behind layer 0's first fragment loads (their latency and the raw rows'
+  // overlap); every other body assembles it here, before anything else
+  const bool ctl_late = CTL && W4T > 0 && !P.has_gru;
   if constexpr (CTL) {
     cq = ctl_q(ctl);
     cv = ctl_view(ctl, CL, row0);
     ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
-    lds_dma_wait();
-    __syncthreads();
-    GO2PI_STAMP(P, tid == 0, 5);
+    if (!ctl_late) {
+      lds_dma_wait();
+      __syncthreads();
+    }
+    GO2PI_STAMP(P, tid == 0 && !ctl_late, 5);
   }
   // plain observation rows with no prologue arithmetic are staged by direct-to-LDS
   // loads (needs whole 64-column chunks to fit the LDS row)
   const bool glds_obs = !CTL && !P.pre_sub && !P.pre_div && !P.pre_mul && !P.pre_clip && ((P.in_pad + 63) & ~63) <= S;
   auto stage_obs = [&](int step) {
     if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
+      if (ctl_late) return;  // (w4_step)
       if constexpr (NW == 4)
         ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
                                 ctl.obs + (size_t)row0 * P.in_dim, tid, NT);
@@ -1546,7 +1568,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     for (int e = tid; e < n4; e += NT) l4[e] = z;
   }
   if (P.has_gru) {
-    __syncthreads();  // bufH zero fill above before the hidden rows land
+    // the zero fill above before the hidden rows land (otherwise no barrier: the
+    // hidden rows' direct-to-LDS loads go out beside the observation's)
+    if (P.zero_fill) __syncthreads();
     if (W4T > 0 && H % 64 == 0) {
       // pipeline: the hidden rows by direct-to-LDS loads, in flight with the
       // observation's (one 64-column chunk per instruction; rows past B read zeros)
@@ -1707,6 +1731,16 @@ int w4_launch(const DevProgram &p, const DevProgram *p_dev, const float *obs, fl
 template <int TPW>
 int w4_launch_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, float *hidden, int batch,
                   void *stream);
+// The generic body's host side, one translation unit per wave count
+// (kernels_gen_w{4,8,16}.hip).
+template <int NW>
+int gen_configure(const DevProgram &p);
+template <int NW>
+int gen_launch(const DevProgram &p, const DevProgram *p_dev, const float *obs, float *act, float *hidden, int batch,
+               int steps, void *stream);
+template <int NW>
+int gen_launch_ctl(const DevProgram &p, const DevProgram *p_dev, const DevCtl &ctl, float *hidden, int batch,
+                   void *stream);
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0, int ACTC = -1, int NHC = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram *__restrict__ Pd,

@@ -358,29 +358,15 @@ size_t gemv_lds_bytes(const DevProgram &p, int layer) {
   return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * p.L[layer].K_pad + GEMV_WAVES * GO2PI_SMALL_MAXB * 16);
 }
 
-template <int NW, int RNN>
-static hipError_t set_fused_lds(const DevProgram &p) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_kernel<NW, 0, 0, 0, RNN>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds_bytes(p, NW));
-  if (e != hipSuccess) return e;
-  const size_t ctl = fused_ctl_lds_bytes(p, NW);
-  if (ctl > 160 * 1024) return hipSuccess;  // controller tick unavailable for this width (launch fails loudly)
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&policy_fused_ctl_kernel<NW, 0, 0, 0, RNN>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)ctl);
-}
-
-// The generic-body instantiation for `waves` (the 4-wave pipeline's live in
-// kernels_w4_t{2,4,8}.hip, one translation unit per tiles-per-wave: w4_*<TPW>).
-template <int NW, int RNN>
-struct FusedTag {};
-// RNN: the recurrent cell (0 none / GRU, 1 LSTM)
+// The generic body's instantiations live in kernels_gen_w{4,8,16}.hip and the 4-wave
+// pipeline's in kernels_w4_t{2,4,8}.hip (one translation unit each, compiled in
+// parallel): gen_*<waves> / w4_*<tiles per wave>.
 template <class F>
-static void with_fused(const DevProgram &p, int waves, F &&f) {
-  const bool lstm = p.has_gru && p.gru.cell == 1;
+static int with_waves(int waves, F &&f) {
   switch (waves) {
-    case 4: lstm ? f(FusedTag<4, 1>{}) : f(FusedTag<4, 0>{}); return;
-    case 16: lstm ? f(FusedTag<16, 1>{}) : f(FusedTag<16, 0>{}); return;
-    default: lstm ? f(FusedTag<8, 1>{}) : f(FusedTag<8, 0>{}); return;
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 16: return f(std::integral_constant<int, 16>{});
+    default: return f(std::integral_constant<int, 8>{});
   }
 }
 
@@ -395,13 +381,10 @@ static int with_w4(const DevProgram &p, F &&f) {
 
 int configure_kernels(const DevProgram &p, int waves) {
   hipError_t e = hipSuccess;
-  if (waves == 4 && p.w4_tpw) {
+  if (waves == 4 && p.w4_tpw)
     e = (hipError_t)with_w4(p, [&](auto t) { return w4_configure<decltype(t)::value>(p); });
-  } else {
-    with_fused(p, waves, [&](auto tag) {
-      e = [&]<int NW, int RNN>(FusedTag<NW, RNN>) { return set_fused_lds<NW, RNN>(p); }(tag);
-    });
-  }
+  else
+    e = (hipError_t)with_waves(waves, [&](auto w) { return gen_configure<decltype(w)::value>(p); });
   if (e != hipSuccess) return (int)e;
   int gmax = 0;
   for (int l = 0; l < p.nl; ++l) gmax = std::max(gmax, (int)gemv_lds_bytes(p, l));
@@ -417,16 +400,9 @@ int launch_policy_fused(const DevProgram &p, const DevProgram *p_dev, int waves,
     return with_w4(p, [&](auto t) {
       return w4_launch<decltype(t)::value>(p, p_dev, obs, act, hidden, batch, steps, stream);
     });
-  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
-  const size_t lds = fused_lds_bytes(p, waves);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(p, waves, [&](auto tag) {
-    [&]<int NW, int RNN>(FusedTag<NW, RNN>) {
-      hipLaunchKernelGGL((policy_fused_kernel<NW, 0, 0, 0, RNN>), grid, dim3(NW * 64), lds, s, p_dev, obs, act,
-                         hidden, batch, steps);
-    }(tag);
+  return with_waves(waves, [&](auto w) {
+    return gen_launch<decltype(w)::value>(p, p_dev, obs, act, hidden, batch, steps, stream);
   });
-  return (int)hipGetLastError();
 }
 
 int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int waves, const DevCtl &ctl,
@@ -436,15 +412,9 @@ int launch_policy_fused_ctl(const DevProgram &p, const DevProgram *p_dev, int wa
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   if (waves == 4 && p.w4_tpw)
     return with_w4(p, [&](auto t) { return w4_launch_ctl<decltype(t)::value>(p, p_dev, ctl, hidden, batch, stream); });
-  const dim3 grid((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  with_fused(p, waves, [&](auto tag) {
-    [&]<int NW, int RNN>(FusedTag<NW, RNN>) {
-      hipLaunchKernelGGL((policy_fused_ctl_kernel<NW, 0, 0, 0, RNN>), grid, dim3(NW * 64), lds, s, p_dev, ctl,
-                         hidden, batch);
-    }(tag);
+  return with_waves(waves, [&](auto w) {
+    return gen_launch_ctl<decltype(w)::value>(p, p_dev, ctl, hidden, batch, stream);
   });
-  return (int)hipGetLastError();
 }
 
 int launch_gemv_layer(const DevProgram &p, int layer, const float *x, int x_stride, float *y, int y_stride,

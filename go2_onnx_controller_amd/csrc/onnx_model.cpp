@@ -15,6 +15,7 @@
 #include "onnx_model.hpp"
 
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -117,9 +118,11 @@ struct Tensor {
   std::vector<float> f;  // FLOAT data
   std::vector<int64_t> i; // INT64 data (Unsqueeze/Squeeze axes in opset 13+)
   int dtype = 0;
+  // -1 for a negative dim or a product past int64 (never equal to a real element count)
   int64_t numel() const {
     int64_t n = 1;
-    for (auto d : dims) n *= d;
+    for (auto d : dims)
+      if (d < 0 || __builtin_mul_overflow(n, d, &n)) return -1;
     return n;
   }
 };
@@ -139,7 +142,7 @@ Tensor parse_tensor(Span s) {
           size_t n = f.s.n / 4;
           size_t o = t.f.size();
           t.f.resize(o + n);
-          std::memcpy(t.f.data() + o, f.s.p, n * 4);
+          if (n) std::memcpy(t.f.data() + o, f.s.p, n * 4);
         } else {
           t.f.push_back(as_f32(f.v));
         }
@@ -154,10 +157,11 @@ Tensor parse_tensor(Span s) {
     if (t.dtype == 1) {
       if (raw.n % 4) fail("raw_data size of " + t.name);
       t.f.resize(raw.n / 4);
-      std::memcpy(t.f.data(), raw.p, raw.n);  // unaligned source
+      if (raw.n) std::memcpy(t.f.data(), raw.p, raw.n);  // unaligned source
     } else if (t.dtype == 7) {
+      if (raw.n % 8) fail("raw_data size of " + t.name);
       t.i.resize(raw.n / 8);
-      std::memcpy(t.i.data(), raw.p, raw.n);
+      if (raw.n) std::memcpy(t.i.data(), raw.p, raw.n);
     }
   }
   if (t.dtype == 1 && int64_t(t.f.size()) != t.numel()) fail("element count mismatch in " + t.name);
@@ -211,7 +215,7 @@ Node parse_node(Span s) {
             if (g.wt == 2) {
               size_t k = g.s.n / 4, o = a.floats.size();
               a.floats.resize(o + k);
-              std::memcpy(a.floats.data() + o, g.s.p, k * 4);
+              if (k) std::memcpy(a.floats.data() + o, g.s.p, k * 4);
             } else a.floats.push_back(as_f32(g.v));
           } else if (g.no == 8) packed_varints(g, a.ints);
         }
@@ -419,7 +423,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
     if (nd.op == "Gemm") {
       if (nd.in[0] != cur) fail("Gemm: activation must be input A");
       if (nd.iattr("transA", 0)) fail("Gemm transA=1 unsupported");
-      const Tensor &B = init(nd.in[1]);
+      const Tensor &B = init(nd.in.at(1));
       if (B.dims.size() != 2) fail("Gemm: B must be 2-D");
       const bool tb = nd.iattr("transB", 0) != 0;
       const float alpha = nd.fattr("alpha", 1.f), beta = nd.fattr("beta", 1.f);
@@ -447,7 +451,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       pending_bias_ok = true;
     } else if (nd.op == "MatMul") {
       if (nd.in[0] != cur) fail("MatMul: activation must be the left operand");
-      const Tensor &B = init(nd.in[1]);
+      const Tensor &B = init(nd.in.at(1));
       if (B.dims.size() != 2) fail("MatMul: weight must be 2-D");
       Dense d;
       d.K = int(B.dims[0]);
@@ -542,7 +546,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       // pass-through on [B, F]
     } else if (nd.op == "Unsqueeze") {
       // must feed the recurrent cell: X [1, B, I]
-      const std::string u = nd.out[0];
+      const std::string u = nd.out.at(0);
       auto ci = consumers.find(u);
       if (ci == consumers.end() || ci->second.size() != 1 ||
           (nodes[ci->second[0]].op != "GRU" && nodes[ci->second[0]].op != "LSTM"))
@@ -564,6 +568,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
         fail(op + ": W must be [1, " + std::to_string(g.G) + "H, I] (one direction)");
       g.H = int(R.dims.at(2));
       g.I = int(W.dims[2]);
+      if (R.dims.size() != 3 || R.dims[0] != 1 || g.H <= 0 || g.I <= 0) fail(op + ": R must be [1, G*H, H], H > 0");
       if (W.dims[1] != g.G * g.H || R.dims[1] != g.G * g.H) fail(op + ": gate dims mismatch");
       g.lbr = lstm ? 0 : int(nd.iattr("linear_before_reset", 0));
       g.W = W.f;
@@ -680,6 +685,78 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   if (is.size() >= 2 && is[1] > 0 && is[1] != m.in_dim) fail("input feature dim disagrees with weights");
   if (os.size() >= 2 && os[1] > 0 && os[1] != m.out_dim) fail("output feature dim disagrees with weights");
   return m;
+}
+
+namespace {
+
+std::string json_num(double v) {
+  if (std::isnan(v)) return "null";
+  if (std::isinf(v)) return v > 0 ? "1e308" : "-1e308";
+  char t[64];
+  std::snprintf(t, sizeof t, "%.17g", v);
+  return t;
+}
+
+// a JSON string literal (names come from the file: quotes, backslashes and control bytes escaped)
+std::string json_str(const std::string &s) {
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += (char)c;
+    } else if (c < 0x20 || c >= 0x7F) {
+      char t[8];
+      std::snprintf(t, sizeof t, "\\u%04x", c);
+      o += t;
+    } else {
+      o += (char)c;
+    }
+  }
+  return o + "\"";
+}
+
+double sum_of(const std::vector<float> &v) {
+  double s = 0;
+  for (float x : v) s += x;
+  return s;
+}
+
+std::string io_json(const std::vector<IoInfo> &v) {
+  std::string s = "[";
+  for (size_t i = 0; i < v.size(); ++i) {
+    s += (i ? "," : "") + std::string("{\"name\":") + json_str(v[i].name) + ",\"shape\":[";
+    for (size_t d = 0; d < v[i].shape.size(); ++d) s += (d ? "," : "") + std::to_string(v[i].shape[d]);
+    s += "]}";
+  }
+  return s + "]";
+}
+
+}  // namespace
+
+std::string inspect_json(const Model &m) {
+  std::string j = "{\"ir_version\":" + std::to_string(m.ir_version) + ",\"opset\":" + std::to_string(m.opset) +
+                  ",\"producer\":" + json_str(m.producer) + ",\"inputs\":" + io_json(m.inputs) +
+                  ",\"outputs\":" + io_json(m.outputs) + ",\"in_dim\":" + std::to_string(m.in_dim) +
+                  ",\"out_dim\":" + std::to_string(m.out_dim) + ",\"layers\":[";
+  for (size_t l = 0; l < m.layers.size(); ++l) {
+    const auto &d = m.layers[l];
+    j += (l ? "," : "") + std::string("{\"K\":") + std::to_string(d.K) + ",\"N\":" + std::to_string(d.N) +
+         ",\"act\":" + std::to_string(d.act) + ",\"alpha\":" + json_num(d.alpha) + ",\"beta\":" + json_num(d.beta) +
+         ",\"w_sum\":" + json_num(sum_of(d.W)) + ",\"b_sum\":" + json_num(sum_of(d.b)) + "}";
+  }
+  j += "],\"gru\":";
+  if (m.has_gru)
+    j += "{\"cell\":\"" + std::string(m.gru.cell ? "LSTM" : "GRU") + "\",\"I\":" + std::to_string(m.gru.I) +
+         ",\"H\":" + std::to_string(m.gru.H) + ",\"lbr\":" + std::to_string(m.gru.lbr) +
+         ",\"w_sum\":" + json_num(sum_of(m.gru.W)) + ",\"r_sum\":" + json_num(sum_of(m.gru.R)) +
+         ",\"b_sum\":" + json_num(sum_of(m.gru.Wb) + sum_of(m.gru.Rb)) + "}";
+  else
+    j += "null";
+  j += ",\"pre_sub\":" + std::to_string(m.pre_sub.size()) + ",\"pre_div\":" + std::to_string(m.pre_div.size()) +
+       ",\"pre_mul\":" + std::to_string(m.pre_mul.size()) + ",\"pre_clip\":[" + json_num(m.pre_lo) + "," +
+       json_num(m.pre_hi) + "],\"clip\":[" + json_num(m.clip_lo) + "," + json_num(m.clip_hi) +
+       "],\"post_scale\":" + json_num(m.post_scale) + "}";
+  return j;
 }
 
 }  // namespace go2pi

@@ -73,4 +73,10 @@ struct Model {
 // unsupported graphs.
 Model parse_onnx(const uint8_t *data, size_t n);
 
+// The loader's view of a model as JSON (go2pi_inspect_model): I/O, dims, each
+// layer's activation and weight / bias checksums, the recurrent cell, the
+// prologue / epilogue. Host-only (no device): tests/cpp/fuzz_loader.cpp drives
+// parse_onnx + inspect_json under ASan / UBSan.
+std::string inspect_json(const Model &m);
+
 }  // namespace go2pi

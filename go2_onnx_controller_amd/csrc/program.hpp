@@ -200,4 +200,12 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
                     unsigned *done, unsigned long long idle_ticks, const DevCtl *ctl, unsigned long long *hgran,
                     float *hidden, const unsigned *yield, void *stream);
 
+// The single-workgroup resident form (resident.hip policy_resident1_kernel, r04):
+// dense policies of <= 4 layers whose weights fit one CU's registers, at most 16
+// outputs. Same request / answer / leave protocol as launch_resident's act() form.
+bool resident1_fits(const DevProgram &p);
+int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
+                     unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
+                     const unsigned *yield, void *stream);
+
 }  // namespace go2pi

@@ -738,6 +738,229 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   }
 }
 
+// ---------------------------------------------------------------------------
+// policy_resident1_kernel — the resident act() in ONE workgroup (r04), for dense
+// policies whose weights fit one CU's registers: the shipped 98->128^3->12 model is
+// 47,244 parameters (189 KB); a CU holds 512 KB of VGPRs. The multi-workgroup form
+// above spends most of a batch-1 request on hops between workgroups (mirror 1.0 us,
+// each layer hand-off 1.2 us: profiles/r03_res_timeline.json); here every layer is
+// an in-workgroup reduction behind one s_barrier, with no granule, no mirror and no
+// other CU involved:
+//
+//  * 16 waves; dense layer l gives each output n a group of G_l adjacent lanes of
+//    one wave (G_l = the largest power of two with N_pad * G_l <= the threads, at
+//    most 64), lane s of the group owns the input float4s k4 = s + G_l * f, f <
+//    F_l <= R1_FMAX. Those F_l weight float4s sit in the lane's registers for the
+//    kernel's life (loaded once from the packed fragments, program.hpp);
+//  * per request and row: F_l broadcast ds_read_b128 of the input row, 4 F_l fmas
+//    in two chains, the group's sum by DPP row permutes (quad xor 1, quad xor 2,
+//    half-row mirror, row mirror, then cross-row shuffles for G > 16), and the
+//    group's lane 0 adds the bias, applies the activation and writes the output
+//    to the other LDS row buffer; one lds_barrier per layer;
+//  * the final layer runs on waves 1..15 only, so wave 0 — the one that polls the
+//    host for the next request — has no PCIe store of the answer in flight ahead of
+//    its poll loads (a wave's memory ops complete in order);
+//  * the request / answer protocol is the multi-workgroup form's: wave 0 polls the
+//    header and observation granules in pinned host memory (wait_request), the
+//    answer goes back as {epoch, value} action granules the host checks itself.
+// Summation order: per output, two fma chains over its lane's k (f even / odd),
+// then the fixed DPP tree over the group: deterministic, not bit-identical to the
+// launch path's MFMA order (both within the 1e-5 contract of the fp64 oracle).
+constexpr int R1_THREADS = 1024;
+constexpr int R1_LMAX = 4;  // dense layers
+constexpr int R1_FMAX = 4;  // weight float4s per lane per layer (16 floats)
+
+// lanes per output for a layer of n_pad outputs over `threads` lanes
+__host__ __device__ constexpr int r1_group(int n_pad, int threads) {
+  int g = 64;
+  while (g > 1 && n_pad * g > threads) g >>= 1;
+  return g;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over the aligned group of G lanes (G a power of two <= 64); every lane of the
+// group gets the total
+__device__ __forceinline__ float r1_group_sum(float v, int G) {
+  if (G >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]: lane ^ 1
+  if (G >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]: lane ^ 2
+  if (G >= 8) v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8
+  if (G >= 16) v += dpp_f<0x140>(v); // row_mirror: the other 8 of the row
+  if (G >= 32) v += __shfl_xor(v, 16);
+  if (G >= 64) v += __shfl_xor(v, 32);
+  return v;
+}
+
+bool resident1_fits(const DevProgram &p) {
+  if (p.has_gru || p.nl < 1 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
+  for (int l = 0; l < p.nl; ++l) {
+    const int thr = l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS;
+    const int G = r1_group(p.L[l].N_pad, thr);
+    if (p.L[l].N_pad * G > thr) return false;
+    if ((p.L[l].K_pad + 4 * G - 1) / (4 * G) > R1_FMAX) return false;
+  }
+  return true;
+}
+
+template <int LMAX, int FMAX>
+__global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevProgram *__restrict__ Pd,
+                                                                      const u64 *req, u64 *actg, unsigned *err,
+                                                                      unsigned *done, u64 idle_ticks,
+                                                                      const unsigned *yield) {
+  const DevProgram &P = *Pd;
+  extern __shared__ float4 lds4[];
+  const int S = P.lds_stride;
+  float *xa = reinterpret_cast<float *>(lds4);           // [8][S] layer input rows
+  float *xb = xa + GO2PI_SMALL_MAXB * S;                 // [8][S]
+  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch
+  float *obsv = reinterpret_cast<float *>(st + 4);       // [8][in_dim] the request's observation
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = 0;  // (RES_STAMP's workgroup index)
+  (void)g;
+  const int nl = P.nl, in_dim = P.in_dim, nout = P.out_dim;
+  // this lane's weight float4s of every layer (and, on a group's lane 0, the bias of
+  // its output), in registers for the kernel's life; the layers' other fields are
+  // re-read from the program (scalar cache) per request
+  float4 w[LMAX][FMAX];
+  float bias[LMAX];
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l) {
+    bias[l] = 0.f;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) w[l][f] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (l < nl) {
+      const DevLayer &L = P.L[l];
+      const bool lastl = l == nl - 1;
+      const int G = r1_group(L.N_pad, lastl ? R1_THREADS - 64 : R1_THREADS);
+      const int t = lastl ? tid - 64 : tid;  // the final layer skips wave 0 (the poller)
+      const int n = t / G, sl = t % G;
+      if (t >= 0 && n < L.N_pad) {
+        const int T = L.N_pad >> 4;
+        const float4 *W = reinterpret_cast<const float4 *>(L.w);
+#pragma unroll
+        for (int f = 0; f < FMAX; ++f) {
+          const int k = 4 * (sl + G * f);
+          if (k < L.K_pad) w[l][f] = W[((size_t)(k >> 4) * T + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2)];
+        }
+        if (sl == 0) bias[l] = L.bias[n];
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights are in registers before the first wait
+  const unsigned y0 = yield ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                            : 0u;
+  unsigned last = 0, nreq = 0;
+  (void)nreq;
+  for (;;) {
+    if (wave == 0) {
+      int leave = 0, B = 0;
+      unsigned e = 0, word = 0;
+      wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
+                                              yield, y0);
+      RES_STAMP(0);
+      if (lane == 0) {
+        st[0] = leave;
+        st[1] = (int)e;
+        st[2] = B;
+      }
+    }
+    lds_barrier();
+    if (st[0]) break;
+    const unsigned e = (unsigned)st[1];
+    const int B = st[2];
+    last = e;
+    // layer 0's input rows: the observation through the prologue, zeros past in_dim
+    {
+      const int K0 = P.L[0].K_pad;
+      for (int i = tid; i < B * K0; i += R1_THREADS) {
+        const int b = i / K0, k = i - b * K0;
+        xa[b * S + k] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
+      }
+    }
+    lds_barrier();
+    RES_STAMP(1);
+    float *X = xa, *Y = xb;
+#pragma unroll
+    for (int l = 0; l < LMAX; ++l) {
+      if (l < nl) {
+        const DevLayer &L = P.L[l];
+        const bool lastl = l == nl - 1;
+        const int G = r1_group(L.N_pad, lastl ? R1_THREADS - 64 : R1_THREADS), K = L.K_pad;
+        const int t = lastl ? tid - 64 : tid;
+        const int n = t / G, sl = t % G;
+        const bool mine = t >= 0 && n < L.N_pad;
+        for (int b = 0; b < B; ++b) {
+          float a0 = 0.f, a1 = 0.f;
+          if (mine) {
+            const float *xr = X + b * S;
+#pragma unroll
+            for (int f = 0; f < FMAX; ++f) {
+              const int k = 4 * (sl + G * f);
+              if (k < K) {
+                const float4 x = *reinterpret_cast<const float4 *>(xr + k);
+                float &a = (f & 1) ? a1 : a0;
+                a = fmaf(x.x, w[l][f].x, a);
+                a = fmaf(x.y, w[l][f].y, a);
+                a = fmaf(x.z, w[l][f].z, a);
+                a = fmaf(x.w, w[l][f].w, a);
+              }
+            }
+          }
+          // (lanes past the layer's outputs, and the final layer's wave 0, join the
+          // group sums with zeros: the DPP tree runs on whole rows)
+          const float v = r1_group_sum(a0 + a1, G);
+          if (mine && sl == 0) {
+            const float y = act_fn(L.act, L.alpha, L.beta, v + bias[l]);
+            if (!lastl) Y[b * S + n] = y;
+            else if (n < nout)
+              __hip_atomic_store(actg + (size_t)b * nout + n, ((u64)e << 32) | __float_as_uint(post_fn(P, y)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+        if (!lastl) {
+          lds_barrier();
+          if (l < 6) RES_STAMP(2 + l);  // layer l's outputs in LDS
+          float *t = X;
+          X = Y;
+          Y = t;
+        }
+      }
+    }
+    RES_STAMP(8);  // answer issued (this wave's)
+    ++nreq;
+  }
+  if (tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+size_t resident1_lds_bytes(const DevProgram &p) {
+  return sizeof(float) * (2 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim);
+}
+
+int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
+                     unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
+                     const unsigned *yield, void *stream) {
+  if (!resident1_fits(p)) return (int)hipErrorInvalidValue;
+  const size_t lds = resident1_lds_bytes(p);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  auto kern = policy_resident1_kernel<R1_LMAX, R1_FMAX>;
+  if (lds > 64 * 1024) {
+    const hipError_t a =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (a != hipSuccess) return (int)a;
+  }
+  hipLaunchKernelGGL(kern, dim3(1), dim3(R1_THREADS), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
+                     err, done, idle_ticks, yield);
+  return (int)hipGetLastError();
+}
+
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
                     unsigned long long *actg,
                     unsigned long long *gran, int gstride, unsigned long long *mirror, unsigned *err,

@@ -7,8 +7,8 @@ Needs a library whose resident kernel records wall-clock stamps
   cd go2_onnx_controller_amd/csrc && hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 \\
       -I../../include -DGO2PI_DIAG_RESCLK -c resident.hip -o ../lib/diag/resident_clk.o && \\
   hipcc -shared -fPIC --offload-arch=gfx950 -o ../lib/diag/libgo2pi_resclk.so ../lib/kernels.o \\
-      ../lib/kernels_w4_t2.o ../lib/kernels_w4_t4.o ../lib/kernels_w4_t8.o ../lib/diag/resident_clk.o \\
-      ../lib/engine.o ../lib/onnx_model.o
+      ../lib/kernels_w4_t2.o ../lib/kernels_w4_t4.o ../lib/kernels_w4_t8.o ../lib/kernels_gen_w4.o \\
+      ../lib/kernels_gen_w8.o ../lib/kernels_gen_w16.o ../lib/diag/resident_clk.o ../lib/engine.o ../lib/onnx_model.o
 
   GO2PI_LIB=$PWD/go2_onnx_controller_amd/lib/diag/libgo2pi_resclk.so python3 tools/res_timeline.py
 
@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--model", default="go2_mlp_512")
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "res_timeline.json"))
+    ap.add_argument("--form", choices=["multi", "one"], default="multi",
+                    help="the resident kernel the engine runs: multi-workgroup (policy_resident_kernel) or the "
+                         "single-workgroup policy_resident1_kernel (r04; GO2PI_RES_MULTI=1 forces multi)")
     args = ap.parse_args()
     os.environ["GO2PI_DIAG_STAMPS"] = "1"
     import numpy as np
@@ -56,6 +59,8 @@ def main():
             ts.append((time.perf_counter_ns() - t0) / 1e3)
         st = e.diag_stamps(512 * 32).astype(np.int64).reshape(512, 32)  # syncs: waits for the idle exit
     ts.sort()
+    if args.form == "one":
+        return one_workgroup(args, st, ts, np)
     rows = st[(st[:, 0] > 0) & (st[:, 9] > 0)]
     base = rows[:, 0:1]
     rel = (rows - base) * 10.0 / 1e3  # us
@@ -80,6 +85,34 @@ def main():
            "host_p99_us": ts[int(len(ts) * 0.99)], "median_us_from_wg0_seen": med,
            "median_done_to_next_seen_us": round(float(np.median(gaps)), 3),
            "shader_clock_ghz_median": round(float(np.median(ghz)), 3)}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+def one_workgroup(args, st, ts, np):
+    """policy_resident1_kernel stamps (100 MHz wall clock): 0 request seen by the
+    polling wave, 1 layer 0's input staged, 2 + l layer l's outputs in LDS (hidden
+    layers), 8 the answer's granule stores issued (wave 1's head output)."""
+    rows = st[(st[:, 0] > 0) & (st[:, 8] > 0)]
+    rel = (rows - rows[:, 0:1]) * 10.0 / 1e3
+    names = {1: "input staged", 8: "answer issued"}
+    for l in range(6):
+        names[2 + l] = f"layer{l} done"
+    med, prev = {}, 0.0
+    for s_ in sorted(names):
+        ok = rows[:, s_] > 0
+        if ok.sum() < len(rows) // 2:
+            continue
+        m = float(np.median(rel[ok, s_]))
+        med[names[s_]] = {"at_us": round(m, 3), "step_us": round(m - prev, 3)}
+        prev = m
+    gaps = (rows[1:, 0] - rows[:-1, 8]) * 10.0 / 1e3
+    out = {"model": args.model, "kernel": "policy_resident1_kernel (one workgroup)",
+           "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2], "host_p99_us": ts[int(len(ts) * 0.99)],
+           "median_from_request_seen": med,
+           "median_answer_to_next_seen_us": round(float(np.median(gaps)), 3)}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump(out, fh, indent=1)
