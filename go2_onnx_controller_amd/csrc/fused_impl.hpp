@@ -807,9 +807,11 @@ __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int 
 // fragments, waits for everything OLDER than them (the LDS-DMA), then barriers,
 // so the fragment latency overlaps the staging. Gate biases are added after the
 // contraction (accumulators start at zero), so their loads wait nowhere.
-template <int GT>
+// mid(): called between the contraction and the epilogue (the caller issues the next
+// stage's first loads there, so their latency overlaps the gate math).
+template <int GT, class Mid>
 __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
-                                       int lane, float4 (&hn)[GT], unsigned long long *st = nullptr) {
+                                       int lane, float4 (&hn)[GT], unsigned long long *st, Mid &&mid) {
   GO2PI_STAMP_AT(st, wave == 0 && lane == 0, 43);  // GRU stage marks (wave 0): 43 entry, 44 contraction, 45 epilogue
   constexpr int NF = 3 * GT;  // gate fragments per chunk
   constexpr int NM = 4 * NF;  // MFMAs per chunk
@@ -921,6 +923,7 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
   if ((Cxe & 3) == 3) run(std::integral_constant<int, 1>{});
   else run(std::integral_constant<int, 0>{});
   GO2PI_STAMP_AT(st, wave == 0 && lane == 0, 44);
+  mid();
   float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
@@ -948,9 +951,9 @@ __device__ __forceinline__ void w4_gru(const DevGru &G, const float *X, const fl
 // state c of exactly those units lives in the caller's registers (c, in / out):
 // it is elementwise, so no other wave ever needs it and across the ticks of a
 // sequence it never leaves the CU. h' goes to Y rows and to hn.
-template <int GT>
+template <int GT, class Mid>
 __device__ __forceinline__ void w4_lstm(const DevGru &G, const float *X, const float *Hs, float *Y, int xs, int wave,
-                                        int lane, float4 (&hn)[GT], float4 (&c)[GT]) {
+                                        int lane, float4 (&hn)[GT], float4 (&c)[GT], Mid &&mid) {
   constexpr int NF = 4 * GT;  // gate fragments per chunk
   constexpr int NM = 4 * NF;  // MFMAs per chunk
   const int Cx = G.I_pad >> 4, Ch = G.H >> 4, H = G.H;
@@ -1045,6 +1048,7 @@ __device__ __forceinline__ void w4_lstm(const DevGru &G, const float *X, const f
   };
   if ((Cxe & 3) == 3) run(std::integral_constant<int, 1>{});
   else run(std::integral_constant<int, 0>{});
+  mid();
   float *yrow = Y + (lane & 15) * xs + t0 * 16 + u0;
 #pragma unroll
   for (int i = 0; i < GT; ++i) {
@@ -1111,7 +1115,21 @@ __device__ __forceinline__ const float *w4_layer_w(const W4Hot &h, int l) {
   return h.l0w + (size_t)(h.c0 + (l - 1) * CH) * CH * 256;
 }
 
+// Layer 0's first RD chunks of the wave's TPW tiles into the register ring (slots
+// K0S ..): the loads w4_step starts a step with.
+template <int TPW, int C0M>
+__device__ __forceinline__ void w4_prefill(const float *l0w, float4 (&f)[4][TPW], int wave, int lane) {
+  constexpr int RD = GO2PI_W4_RD(TPW), CSB = 4 * TPW * 1024, K0S = (4 - C0M) & 3;
+  const WStream w0(l0w);
+#pragma unroll
+  for (int d = 0; d < RD; ++d)
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = w0.ld(((wave * TPW + i) * 64 + lane) * 16, d * CSB);
+}
+
 // One policy step of the pipeline (the observation tile is being staged into bufA).
+// pre: the ring already filled by w4_prefill and the biases' direct-to-LDS copy
+// already issued (a recurrent policy does both behind its cell's contraction).
 // X0: layer 0's input rows (the observation tile, or a GRU's h'); Y0: the other
 // activation buffer (layer 0's outputs). PL: no action epilogue (post_fn is the
 // identity: the lean kernel). C0M: layer 0's k-chunk count mod 4 (0, or 3 for
@@ -1122,7 +1140,7 @@ template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1, int NHC = 
 __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, float *X0, float *Y0, int S,
                                         f32x4 *scratch, int *flags, float *lbias, int &ep, int wave, int lane,
                                         float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
-                                        const CtlLds &CL, int step) {
+                                        const CtlLds &CL, int step, const float4 (&ring)[4][TPW], bool pre) {
   W4Hot hot = hot0;
   constexpr int RD = GO2PI_W4_RD(TPW);
   constexpr int CH = 4 * TPW;     // k-chunks of every layer after the first (= output tiles of a hidden layer)
@@ -1150,16 +1168,17 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
   // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
   // weight stream, whose waits would otherwise cover them); the head's bias to registers
-  if (step == 0) glds_copy(lbias, hot.bpack, hot.nbias, wave, lane, 4);
+  if (step == 0 && !pre) glds_copy(lbias, hot.bpack, hot.nbias, wave, lane, 4);
   float4 hbv[1];  // the head's bias: fetched with the head's fragments (load_head)
   float4 f[4][TPW];
   asm volatile("" ::: "memory");  // the DMA and bias loads stay ahead of the ring's first loads
-  {
-    const WStream w0(hot.l0w);
+  if (pre) {
 #pragma unroll
     for (int d = 0; d < RD; ++d)
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = w0.ld(vo[i], d * CSB);
+      for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = ring[(K0S + d) & 3][i];
+  } else {
+    w4_prefill<TPW, C0M>(hot.l0w, f, wave, lane);
   }
   if constexpr (PL) {
     // the lean kernel: the program's remaining fields are loaded only now, behind the
@@ -1412,6 +1431,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
   const int nch = (16 * c0 + 63) >> 6;  // 64-column chunks of the observation tile
   int ep = 0;                           // flag epochs published so far (the same in every wave)
+  float4 ring_none[4][TPW];             // (w4_step loads its own ring here)
   for (int step = 0; step < steps; ++step) {
     // wave w stages rows w, w + 4, w + 8, w + 12 in whole 64-column chunks by
     // direct-to-LDS loads
@@ -1430,7 +1450,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
     GO2PI_STAMP(P, tid == 0 && step == 0, 40);
     GO2PI_STAMP(P, tid == 0 && step == 0, 41);
     w4_step<TPW, HT, false, true, C0M, ACTC, NHC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
-                                       CtlLds{}, step);
+                                       CtlLds{}, step, ring_none, false);
   }
   GO2PI_STAMP(P, tid == 0, 2);
   GO2PI_STAMP_RT(P, tid == 0, 3);
@@ -1603,6 +1623,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
       float *X0 = bufA, *Y0 = bufB;
+      float4 ring0[4][W4T > 0 ? W4T : 1];  // layer 0's ring, filled behind a recurrent cell (w4_prefill)
+      bool ring_pre = false;
       if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
         // the pipelined cell (w4_gru / w4_lstm wait for the x / h staging and barrier
         // themselves): h' to bufB, registers, and the carry
@@ -1610,17 +1632,30 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
           constexpr int GT = decltype(gt_k)::value;
           float4 hn[GT];
           constexpr bool lstm = RNN == 1;
+          // layer 0's first fragments (and, on the first step, the hidden layers' biases)
+          // go out between the cell's contraction and its gate math: their L2 / HBM
+          // latency overlaps the epilogue and the hidden-row carry instead of
+          // following them (w4_step then starts from this ring)
+          // (not in the LSTM body with a run-time activation: its ring registers spilled)
+          constexpr bool PREF = !(lstm && ACTC != 1);
+          auto mid = [&] {
+            if constexpr (PREF) {
+              if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
+              w4_prefill<W4T, C0M>(P.l0_w, ring0, wave, lane);
+            }
+          };
           if constexpr (lstm) {
             float4 cr[GT];
 #pragma unroll
             for (int i = 0; i < GT; ++i) cr[i] = creg[i];
-            w4_lstm<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn, cr);
+            w4_lstm<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn, cr, mid);
 #pragma unroll
             for (int i = 0; i < GT; ++i) creg[i] = cr[i];
           } else {
             w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
-                       P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr);
+                       P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, mid);
           }
+          ring_pre = PREF;
           if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's state: once, from registers
             float *hg = hidden + (size_t)(row0 + (lane & 15)) * SW + wave * GT * 16 + ((lane >> 4) << 2);
 #pragma unroll
@@ -1653,9 +1688,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
         X0 = bufB;
         Y0 = bufA;
       }
-      w4_step<W4T, W4H, CTL, false, C0M, ACTC, NHC>(P, w4_hot(P), X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac, cv,
-                                         row0, B, ctl, CL,
-                             step);
+      w4_step<W4T, W4H, CTL, false, C0M, ACTC, NHC>(P, w4_hot(P), X0, Y0, S, scratch, flags, lbias, ep, wave, lane, ac,
+                                                    cv, row0, B, ctl, CL, step, ring0, ring_pre);
       continue;
     }
     lds_dma_wait();  // the observation tile's direct-to-LDS loads

@@ -993,7 +993,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
   if (ctl) tail = (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
   if (rnn)
     tail = (size_t)GO2PI_SMALL_MAXB * (p.gru.I_pad + p.gru.H) + RES_WAVES * 4 * GO2PI_SMALL_MAXB * 16 +
-           2 * GO2PI_SMALL_MAXB + 2 * GO2PI_SMALL_MAXB * 16 * (lstm ? 2 : 1);  // hown (cown), hst (cst)
+           2 * GO2PI_SMALL_MAXB + 4 * GO2PI_SMALL_MAXB * 16;  // hown, cown, hst, cst (laid out for a GRU too)
   const size_t lds = sizeof(float) * (ctl_off + tail);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   auto go = [&](auto kern) {

@@ -25,11 +25,18 @@ def _models(synth_path):
     return {"shipped": SHIPPED, "mlp512": synth_path("go2_mlp_512")}
 
 
-@pytest.mark.parametrize("tiled0", [False, True])
-@pytest.mark.parametrize("name", ["shipped", "mlp512"])
-def test_resident_vs_launch_per_call(synth_path, name, tiled0, monkeypatch):
+# resident forms: "one" the single-workgroup kernel (the default where the weights fit
+# one CU: the shipped model), "multi" the multi-workgroup kernel (GO2PI_RES_MULTI=1 for
+# the shipped model; the only form for mlp512), "tiled0" multi with layer 0 tiled like
+# every other layer (bit-identical to the launch path)
+@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "multi"), ("shipped", "tiled0"),
+                                       ("mlp512", "multi"), ("mlp512", "tiled0")])
+def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import mlp_ref
+    tiled0 = form == "tiled0"
+    if form != "one":
+        monkeypatch.setenv("GO2PI_RES_MULTI", "1")  # read at engine creation
     if tiled0:
         monkeypatch.setenv("GO2PI_RES_TILED0", "1")  # read at each resident launch
     path = _models(synth_path)[name]
