@@ -122,16 +122,21 @@ __device__ __forceinline__ void ctl_lds_load(const CtlLds L, const DevCtl C, int
   if (tid < GO2PI_TILE_ROWS) L.nanf[tid] = 0u;
 }
 
-// Controller parameters the assembly reads, loaded once at kernel start (by
-// value: their scalar loads overlap the input staging instead of following it).
+// Controller parameters and program fields the assembly reads, loaded once (by
+// value: their scalar loads overlap the input staging instead of following it, and
+// none is reloaded after the assembly's stores: measured 8.6K cycles per 16-robot
+// tile when the program's fields were re-read per element).
 struct CtlQ {
   int hist;
   float thr, g0, g1, g2;
+  int in_dim, in_pad;
+  Pro pro;
 };
 
-__device__ __forceinline__ CtlQ ctl_q(const DevCtl C) {
+__device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
   const DevCtlParams &Q = *C.prm;
-  return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2]};
+  return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2], P.in_dim, P.in_pad,
+              pro_of(P)};
 }
 
 // One history block BK of the new observation rows r < nrows, on one wave's
@@ -141,7 +146,7 @@ __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds
                                                float *dst, int ds, float *raw, int lane, int stride = 64) {
   constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
   constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
-  const int H = q.hist, in_dim = P.in_dim;
+  const int H = q.hist, in_dim = q.in_dim;
   const int W = H * d, s0 = H * cum, sh = (H - 1) * d;
   const float rW = 1.f / (float)W;
 #pragma unroll 2
@@ -182,7 +187,7 @@ __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds
       if (BK < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
     }
     if (raw) raw[r * in_dim + k] = v;
-    dst[r * ds + k] = TILE ? prologue(P, v, k) : v;
+    dst[r * ds + k] = TILE ? prologue(q.pro, v, k) : v;
   }
 }
 
@@ -209,14 +214,14 @@ __device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L
       case 6: ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
       default:
         if constexpr (TILE) {  // padding
-          const int in_dim = P.in_dim, pw = P.in_pad - in_dim;
+          const int in_dim = q.in_dim, pw = q.in_pad - in_dim;
           const float rp = 1.f / (float)pw;
           for (int e = lane; e < nrows * pw; e += 64) {
             const int r = (int)(((float)e + 0.5f) * rp);
             dst[r * ds + in_dim + (e - r * pw)] = 0.f;
           }
           for (int r = nrows; r < GO2PI_TILE_ROWS; ++r)
-            for (int k = lane; k < P.in_pad; k += 64) dst[r * ds + k] = 0.f;
+            for (int k = lane; k < q.in_pad; k += 64) dst[r * ds + k] = 0.f;
         }
         break;
     }
@@ -238,15 +243,15 @@ __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const Ctl
   ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   if constexpr (TILE) {  // padding columns [in_dim, in_pad) and rows [nrows, 16)
-    const int in_dim = P.in_dim, pw = P.in_pad - in_dim;
+    const int in_dim = q.in_dim, pw = q.in_pad - in_dim;
     const float rp = 1.f / (float)pw;
     for (int e = tid; e < nrows * pw; e += nt) {
       const int r = (int)(((float)e + 0.5f) * rp);
       dst[r * ds + in_dim + (e - r * pw)] = 0.f;
     }
-    for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * P.in_pad; e += nt) {
-      const int r = nrows + e / P.in_pad;
-      dst[r * ds + (e - (r - nrows) * P.in_pad)] = 0.f;
+    for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * q.in_pad; e += nt) {
+      const int r = nrows + e / q.in_pad;
+      dst[r * ds + (e - (r - nrows) * q.in_pad)] = 0.f;
     }
   }
 }

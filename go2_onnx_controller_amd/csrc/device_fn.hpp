@@ -117,12 +117,28 @@ __device__ __forceinline__ float post_fn(const DevProgram &P, float v) {
   return v * P.scale;
 }
 
-__device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) {
-  if (P.pre_sub) v -= P.pre_sub[P.pre_sub_bcast ? 0 : k];
-  if (P.pre_div) v /= P.pre_div[P.pre_div_bcast ? 0 : k];
-  if (P.pre_mul) v *= P.pre_mul[P.pre_mul_bcast ? 0 : k];
-  if (P.pre_clip) v = clip_nan(v, P.obs_lo, P.obs_hi);
+// The prologue's program fields, read once (by value): loops that store to memory
+// between elements would otherwise reload them, and a reload the compiler cannot
+// prove unaliased by those stores becomes a vector load (an L2 round trip per element).
+struct Pro {
+  const float *sub, *div, *mul;
+  int sub_b, div_b, mul_b, clip;
+  float lo, hi;
+};
+
+__device__ __forceinline__ Pro pro_of(const DevProgram &P) {
+  return Pro{P.pre_sub, P.pre_div, P.pre_mul, P.pre_sub_bcast, P.pre_div_bcast, P.pre_mul_bcast, P.pre_clip,
+             P.obs_lo, P.obs_hi};
+}
+
+__device__ __forceinline__ float prologue(const Pro &q, float v, int k) {
+  if (q.sub) v -= q.sub[q.sub_b ? 0 : k];
+  if (q.div) v /= q.div[q.div_b ? 0 : k];
+  if (q.mul) v *= q.mul[q.mul_b ? 0 : k];
+  if (q.clip) v = clip_nan(v, q.lo, q.hi);
   return v;
 }
+
+__device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) { return prologue(pro_of(P), v, k); }
 
 }  // namespace go2pi

@@ -268,8 +268,9 @@ struct go2pi_engine {
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     std::memset(h_actg, 0, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)model.out_dim);
-    if (!ctl && resident1)
-      hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, stream),
+    if (resident1)
+      hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, ctl,
+                                        stream),
                 "resident launch (one workgroup)");
     else
       hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,

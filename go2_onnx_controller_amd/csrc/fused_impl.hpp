@@ -1206,7 +1206,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     if (ctl_here) {
       wg_barrier_vm<RD * TPW>();
       GO2PI_STAMP(P, threadIdx.x == 0, 5);
-      ctl_assemble_flat<true>(P, CL, ctl_q(ctl), ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
+      ctl_assemble_flat<true>(P, CL, ctl_q(P, ctl), ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
                               ctl.obs + (size_t)row0 * P.in_dim, threadIdx.x, 256);
       lds_barrier();
     }
@@ -1512,7 +1512,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // overlap); every other body assembles it here, before anything else
   const bool ctl_late = CTL && W4T > 0 && !P.has_gru;
   if constexpr (CTL) {
-    cq = ctl_q(ctl);
+    cq = ctl_q(P, ctl);
     cv = ctl_view(ctl, CL, row0);
     ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), P.in_dim, tid, wave, lane, NW);
     if (!ctl_late) {

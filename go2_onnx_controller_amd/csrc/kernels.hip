@@ -185,7 +185,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
   CtlView cv{};
   CtlQ cq{};
   if constexpr (CTL) {
-    cq = ctl_q(ctl);
+    cq = ctl_q(P, ctl);
     cv = ctl_view(ctl, CL, 0);
     if (g < (P.L[0].N_pad >> 4)) {  // layer-0 WGs
       ctl_lds_load(CL, ctl, 0, B, P.in_dim, tid, wave, lane, LAT_WAVES);

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
         if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
         __syncthreads();
-        ctl_assemble_flat<false>(P, CL, ctl_q(C), joy, B, obsv, in_dim, nullptr, tid, RES_WAVES * 64);
+        ctl_assemble_flat<false>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, RES_WAVES * 64);
         __syncthreads();
         if (wave == 0) {  // mirror the assembled observation for the other workgroups
           for (int i = lane; i < B * in_dim; i += 64)
@@ -777,6 +777,14 @@ __host__ __device__ constexpr int r1_group(int n_pad, int threads) {
   return g;
 }
 
+// a uniform value kept in an SGPR as it is (opaque to the optimizer: never reloaded)
+__device__ __forceinline__ int r1_keep(int v) {
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ float r1_keep(float v) { return __int_as_float(r1_keep(__float_as_int(v))); }
+
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -794,6 +802,17 @@ __device__ __forceinline__ float r1_group_sum(float v, int G) {
   return v;
 }
 
+// the per-layer float4 counts of program p, packed as the kernel's FS
+unsigned r1_shape(const DevProgram &p) {
+  unsigned fs = 0;
+  for (int l = 0; l < p.nl && l < R1_LMAX; ++l) {
+    const int thr = l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS;
+    const int G = r1_group(p.L[l].N_pad, thr);
+    fs |= (unsigned)((p.L[l].K_pad + 4 * G - 1) / (4 * G)) << (4 * l);
+  }
+  return fs;
+}
+
 bool resident1_fits(const DevProgram &p) {
   if (p.has_gru || p.nl < 1 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
   for (int l = 0; l < p.nl; ++l) {
@@ -805,18 +824,31 @@ bool resident1_fits(const DevProgram &p) {
   return true;
 }
 
-template <int LMAX, int FMAX>
+// CTL: the controller tick (go2pi_controller_step at batch <= 8), as the multi-
+// workgroup kernel's controller form: the request carries the tick's raw rows
+// (state | joystick | previous obs | previous action, as tagged granules), the
+// observation is assembled here (ctl_fn.hpp), the action post-processed into the
+// pinned staging C names (ctl_store), the new observation rows and NaN flags written,
+// then the done word.
+// FS: weight float4s per lane of each layer, packed as 4-bit fields (layer l in bits
+// 4l..4l+3), so a policy shape gets exactly the registers its layers need (the
+// shipped model: 4, 4, 4, 1); the generic instantiation holds R1_FMAX for every layer.
+template <int LMAX, int FMAX, bool CTL, unsigned FS = 0x4444u>
 __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevProgram *__restrict__ Pd,
                                                                       const u64 *req, u64 *actg, unsigned *err,
                                                                       unsigned *done, u64 idle_ticks,
-                                                                      const unsigned *yield) {
+                                                                      const unsigned *yield, DevCtl C) {
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
   const int S = P.lds_stride;
   float *xa = reinterpret_cast<float *>(lds4);           // [8][S] layer input rows
   float *xb = xa + GO2PI_SMALL_MAXB * S;                 // [8][S]
-  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch
+  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch, [3] word
   float *obsv = reinterpret_cast<float *>(st + 4);       // [8][in_dim] the request's observation
+  // CTL: the LDS image of the tick's inputs (16-byte aligned: q0 is double), then the request rows
+  float *cbase = obsv + (GO2PI_SMALL_MAXB * P.in_dim + 3) / 4 * 4;
+  const CtlLds CL = ctl_lds(cbase, GO2PI_SMALL_MAXB, P.in_dim);
+  float *craw = cbase + ctl_lds_floats(GO2PI_SMALL_MAXB, P.in_dim);  // [B][GO2PI_CTL_RAW + in_dim]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = 0;  // (RES_STAMP's workgroup index)
@@ -832,7 +864,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     bias[l] = 0.f;
 #pragma unroll
     for (int f = 0; f < FMAX; ++f) w[l][f] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (l < nl) {
+    if (l < nl && l < LMAX) {
       const DevLayer &L = P.L[l];
       const bool lastl = l == nl - 1;
       const int G = r1_group(L.N_pad, lastl ? R1_THREADS - 64 : R1_THREADS);
@@ -844,12 +876,36 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
 #pragma unroll
         for (int f = 0; f < FMAX; ++f) {
           const int k = 4 * (sl + G * f);
-          if (k < L.K_pad) w[l][f] = W[((size_t)(k >> 4) * T + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2)];
+          if (f < (int)((FS >> (4 * l)) & 15u) && k < L.K_pad)
+            w[l][f] = W[((size_t)(k >> 4) * T + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2)];
         }
         if (sl == 0) bias[l] = L.bias[n];
       }
     }
   }
+  // every program field a request reads, in registers for the kernel's life: after an
+  // idle wait the scalar cache has lost the program's lines, and each dependent reload
+  // (layer dims -> group size -> addresses; activation kind; the epilogue) is an L2
+  // round trip on the request's path. The empty asm makes each value opaque, so the
+  // compiler keeps it (in an SGPR, or a VGPR lane when it spills) instead of reloading.
+  int lK[LMAX], lNp[LMAX], lact[LMAX];
+  float lal[LMAX], lbe[LMAX];
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l) {
+    const DevLayer &L = P.L[l < nl ? l : 0];
+    lK[l] = r1_keep(L.K_pad);
+    lNp[l] = r1_keep(L.N_pad);
+    lact[l] = r1_keep(L.act);
+    lal[l] = r1_keep(L.alpha);
+    lbe[l] = r1_keep(L.beta);
+  }
+  const int pro_plain = r1_keep((int)(!P.pre_sub && !P.pre_div && !P.pre_mul && !P.pre_clip));
+  const int post_tanh = r1_keep(P.post_tanh);
+  const float clo = r1_keep(P.clip_lo), chi = r1_keep(P.clip_hi), pscale = r1_keep(P.scale);
+  auto post = [&](float v) {
+    if (post_tanh) v = tanhf(v);
+    return clip_nan(v, clo, chi) * pscale;
+  };
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights are in registers before the first wait
   const unsigned y0 = yield ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)
@@ -860,26 +916,57 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     if (wave == 0) {
       int leave = 0, B = 0;
       unsigned e = 0, word = 0;
-      wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
-                                              yield, y0);
+      if constexpr (CTL)
+        wait_request<__HIP_MEMORY_SCOPE_SYSTEM, 3>(req, GO2PI_CTL_RAW + in_dim, last, idle_ticks, craw, err, lane,
+                                                   leave, e, B, word, yield, y0);
+      else
+        wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
+                                                yield, y0);
       RES_STAMP(0);
+      RES_CLOCK(15);
       if (lane == 0) {
         st[0] = leave;
         st[1] = (int)e;
         st[2] = B;
+        st[3] = (int)word;
       }
     }
     lds_barrier();
     if (st[0]) break;
     const unsigned e = (unsigned)st[1];
     const int B = st[2];
+    const unsigned word = (unsigned)st[3];
+    (void)word;
     last = e;
+    CtlView cv{};
+    if constexpr (CTL) {
+      // the request's rows (craw: state | joystick | previous obs | previous action, each B
+      // rows) into the assembly's LDS image, then the observation assembled into obsv
+      const bool joy = (word & GO2PI_RES_JOY) != 0u;
+      const int o_jy = B * GO2PI_CTL_STATE_DIM, o_obs = o_jy + B * GO2PI_CTL_JOY_DIM, o_act = o_obs + B * in_dim;
+      for (int i = tid; i < o_jy; i += R1_THREADS) CL.st[i] = craw[i];
+      for (int i = tid; i < B * GO2PI_CTL_JOY_DIM; i += R1_THREADS) CL.jy[i] = craw[o_jy + i];
+      for (int i = tid; i < B * in_dim; i += R1_THREADS) CL.obs[i] = craw[o_obs + i];
+      for (int i = tid; i < B * GO2PI_CTL_DOF; i += R1_THREADS) CL.act[i] = craw[o_act + i];
+      if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
+      if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
+      __syncthreads();
+      ctl_assemble_flat<false>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, R1_THREADS);
+      DevCtl c = C;
+      if (!joy) c.joy = nullptr;
+      if (!(word & GO2PI_RES_QDES)) c.q_des = nullptr;
+      if (!(word & GO2PI_RES_KP)) c.kp = nullptr;
+      if (!(word & GO2PI_RES_KD)) c.kd = nullptr;
+      cv = ctl_view(c, CL, 0);
+      lds_barrier();
+    }
     // layer 0's input rows: the observation through the prologue, zeros past in_dim
     {
-      const int K0 = P.L[0].K_pad;
+      const int K0 = lK[0];
       for (int i = tid; i < B * K0; i += R1_THREADS) {
         const int b = i / K0, k = i - b * K0;
-        xa[b * S + k] = k < in_dim ? prologue(P, obsv[b * in_dim + k], k) : 0.f;
+        const float v = k < in_dim ? obsv[b * in_dim + k] : 0.f;
+        xa[b * S + k] = (k >= in_dim || pro_plain) ? v : prologue(P, v, k);
       }
     }
     lds_barrier();
@@ -888,12 +975,11 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
 #pragma unroll
     for (int l = 0; l < LMAX; ++l) {
       if (l < nl) {
-        const DevLayer &L = P.L[l];
         const bool lastl = l == nl - 1;
-        const int G = r1_group(L.N_pad, lastl ? R1_THREADS - 64 : R1_THREADS), K = L.K_pad;
+        const int G = r1_group(lNp[l], lastl ? R1_THREADS - 64 : R1_THREADS), K = lK[l];
         const int t = lastl ? tid - 64 : tid;
         const int n = t / G, sl = t % G;
-        const bool mine = t >= 0 && n < L.N_pad;
+        const bool mine = t >= 0 && n < lNp[l];
         for (int b = 0; b < B; ++b) {
           float a0 = 0.f, a1 = 0.f;
           if (mine) {
@@ -901,7 +987,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
 #pragma unroll
             for (int f = 0; f < FMAX; ++f) {
               const int k = 4 * (sl + G * f);
-              if (k < K) {
+              if (f < (int)((FS >> (4 * l)) & 15u) && k < K) {
                 const float4 x = *reinterpret_cast<const float4 *>(xr + k);
                 float &a = (f & 1) ? a1 : a0;
                 a = fmaf(x.x, w[l][f].x, a);
@@ -915,11 +1001,15 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
           // group sums with zeros: the DPP tree runs on whole rows)
           const float v = r1_group_sum(a0 + a1, G);
           if (mine && sl == 0) {
-            const float y = act_fn(L.act, L.alpha, L.beta, v + bias[l]);
+            const float y = act_fn(lact[l], lal[l], lbe[l], v + bias[l]);
             if (!lastl) Y[b * S + n] = y;
-            else if (n < nout)
-              __hip_atomic_store(actg + (size_t)b * nout + n, ((u64)e << 32) | __float_as_uint(post_fn(P, y)),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else if (n < nout) {
+              if constexpr (CTL)
+                ctl_store(cv, b, n, post(y));
+              else
+                __hip_atomic_store(actg + (size_t)b * nout + n, ((u64)e << 32) | __float_as_uint(post(y)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
           }
         }
         if (!lastl) {
@@ -932,6 +1022,15 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
       }
     }
     RES_STAMP(8);  // answer issued (this wave's)
+    RES_CLOCK(14);
+    if constexpr (CTL) {  // the new observation rows and NaN flags, then the done word
+      for (int i = tid; i < B * in_dim; i += R1_THREADS) C.obs[i] = obsv[i];
+      if ((word & GO2PI_RES_STATUS) && tid < B) C.status[tid] = CL.nanf[tid];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     ++nreq;
   }
   if (tid == 0) {
@@ -940,25 +1039,34 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
   }
 }
 
-size_t resident1_lds_bytes(const DevProgram &p) {
-  return sizeof(float) * (2 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + (size_t)GO2PI_SMALL_MAXB * p.in_dim);
+size_t resident1_lds_bytes(const DevProgram &p, bool ctl) {
+  size_t f = 2 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + ((size_t)GO2PI_SMALL_MAXB * p.in_dim + 3) / 4 * 4;
+  if (ctl) f += (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
+  return sizeof(float) * f;
 }
 
 int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
-                     const unsigned *yield, void *stream) {
+                     const unsigned *yield, const DevCtl *ctl, void *stream) {
   if (!resident1_fits(p)) return (int)hipErrorInvalidValue;
-  const size_t lds = resident1_lds_bytes(p);
+  const size_t lds = resident1_lds_bytes(p, ctl != nullptr);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  auto kern = policy_resident1_kernel<R1_LMAX, R1_FMAX>;
-  if (lds > 64 * 1024) {
-    const hipError_t a =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (a != hipSuccess) return (int)a;
-  }
-  hipLaunchKernelGGL(kern, dim3(1), dim3(R1_THREADS), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
-                     err, done, idle_ticks, yield);
-  return (int)hipGetLastError();
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) {
+      const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (a != hipSuccess) return (int)a;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(R1_THREADS), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
+                       err, done, idle_ticks, yield, ctl ? *ctl : DevCtl{});
+    return (int)hipGetLastError();
+  };
+  // the shipped model's shape (98 -> 128^3 -> 12: 4, 4, 4, 1 float4s per lane) has its own
+  // instantiation: the registers it leaves free keep the controller form out of scratch
+  if (p.nl == 4 && r1_shape(p) == 0x1444u)
+    return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true, 0x1444u>)
+               : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false, 0x1444u>);
+  return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true>) : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false>);
 }
 
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,

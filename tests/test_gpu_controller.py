@@ -178,13 +178,18 @@ def test_controller_rejects_non_controller_policy(synth_path):
                               np.zeros((1, 12), np.float32))
 
 
+@pytest.mark.parametrize("form", ["one", "multi"])
 @pytest.mark.parametrize("B", [1, 3, 8])
-def test_controller_ticks_resident(B):
+def test_controller_ticks_resident(B, form, monkeypatch):
     """The resident kernel's controller form (go2pi_opts.resident_ms > 0, batch <= 8):
     same bit-exact observation / action contract, with and without joystick rows,
-    with and without the optional outputs, and switching to and from the act() form."""
+    with and without the optional outputs, and switching to and from the act() form.
+    form: the single-workgroup kernel (the shipped model's default) or the
+    multi-workgroup one (GO2PI_RES_MULTI=1)."""
     from go2_onnx_controller_amd import Engine
     from oracle import controller_ref as cr
+    if form == "multi":
+        monkeypatch.setenv("GO2PI_RES_MULTI", "1")
     pol = _mlp_policy(SHIPPED)
     with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
         obs, act = _run_ticks(e, pol, B, 6, seed=40 + B)
@@ -199,9 +204,12 @@ def test_controller_ticks_resident(B):
             assert rel_err(e.run(x), pol(x)) <= TOL
 
 
-def test_controller_resident_nan_status():
+@pytest.mark.parametrize("form", ["one", "multi"])
+def test_controller_resident_nan_status(form, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import controller_ref as cr
+    if form == "multi":
+        monkeypatch.setenv("GO2PI_RES_MULTI", "1")
     rng = np.random.default_rng(77)
     B = 4
     with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
