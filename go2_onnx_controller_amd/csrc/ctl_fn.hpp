@@ -143,7 +143,15 @@ __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
 // lanes: straight-line code per block (BK is a template parameter).
 template <int BK, bool TILE>
 __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
-                                               float *dst, int ds, float *raw, int lane, int stride = 64) {
+                                               float *dst_, int ds, float *raw_, int lane, int stride = 64) {
+  // the LDS image, the destination tile and the caller's rows never overlap: without
+  // __restrict__ every element's reads waited behind the previous element's stores
+  const float *__restrict__ obs_l = L.obs;
+  const float *__restrict__ st_l = L.st;
+  const float *__restrict__ jy_l = L.jy;
+  const float *__restrict__ act_l = L.act;
+  float *__restrict__ dst = dst_;
+  float *__restrict__ raw = raw_;
   constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
   constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
   const int H = q.hist, in_dim = q.in_dim;
@@ -155,19 +163,19 @@ __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds
     // float product's error is far below that for these sizes (W <= 49 * 16)
     const int r = (int)(((float)e + 0.5f) * rW);
     const int j = e - r * W, k = s0 + j;
-    const float *orow = L.obs + r * in_dim;
+    const float *orow = obs_l + r * in_dim;
     float v;
     if (j < sh) {
       v = orow[k + d];  // std::shift_left by d
     } else {
       const int i = j - sh;
-      const float *st = L.st + r * GO2PI_CTL_STATE_DIM;
+      const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
       if constexpr (BK == 0) {
         v = ctl_gravity(st, q.g0, q.g1, q.g2, i);
       } else if constexpr (BK == 1) {
         v = st[4 + i];  // imu gyroscope (controller.hpp:105-109)
       } else if constexpr (BK == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
-        const float *jy = L.jy + r * GO2PI_CTL_JOY_DIM;
+        const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
         if (!joy || jy[0] == 0.f) v = orow[k];  // the previous tick's vel_cmd_
         else if (i == 0) v = jy[2];             // axes[1]
         else if (i == 2) v = jy[3] * jy[2];     // axes[3] * axes[1]
@@ -180,7 +188,7 @@ __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds
       } else if constexpr (BK == 4) {
         v = st[19 + i];
       } else if constexpr (BK == 5) {
-        v = L.act[r * GO2PI_CTL_DOF + i];  // action_ before act()
+        v = act_l[r * GO2PI_CTL_DOF + i];  // action_ before act()
       } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
         v = st[31 + (i ^ 1)] >= q.thr ? 1.f : 0.f;
       }
@@ -235,13 +243,21 @@ __device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L
 template <bool TILE>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
+  // (GO2PI_DIAG_CLOCK: thread 0's time after each block, slots 50 + block)
   ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 50);
   ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 51);
   ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 52);
   ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 53);
   ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 54);
   ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 55);
   ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 56);
   if constexpr (TILE) {  // padding columns [in_dim, in_pad) and rows [nrows, 16)
     const int in_dim = q.in_dim, pw = q.in_pad - in_dim;
     const float rp = 1.f / (float)pw;

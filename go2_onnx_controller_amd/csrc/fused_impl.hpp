@@ -25,33 +25,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? 1 : ((TPW) >= 4 ? 2 : 3))
 #define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
 
-// Clock stamps (GO2PI_DIAG_CLOCK builds, tools/clock_probe.py): s_memtime (or the
-// 100 MHz s_memrealtime) of a workgroup's phases into P.stamps[block][slot]. In the
-// shipped build the macros are empty: no load, no store, no condition evaluated.
-#ifdef GO2PI_DIAG_CLOCK
-#define GO2PI_STAMP_AT(row, cond, slot)                                  \
-  do {                                                                   \
-    if ((row) && (cond)) (row)[slot] = __builtin_amdgcn_s_memtime();     \
-  } while (0)
-#define GO2PI_STAMP(P, cond, slot) \
-  GO2PI_STAMP_AT((P).stamps ? (P).stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, cond, slot)
-#define GO2PI_STAMP_RT(P, cond, slot)                                                                       \
-  do {                                                                                                      \
-    if ((P).stamps && (cond)) (P).stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define GO2PI_STAMP_AT(row, cond, slot) \
-  do {                                  \
-    (void)sizeof(row);                  \
-  } while (0)
-#define GO2PI_STAMP(P, cond, slot) \
-  do {                             \
-  } while (0)
-#define GO2PI_STAMP_RT(P, cond, slot) \
-  do {                                \
-  } while (0)
-#endif
-
 // Diagnostic ablation builds only (tools/bound_probe.sh; outputs are wrong by design):
 //   GO2PI_DIAG_NOMFMA  — replace each MFMA by one VALU fma (keeps the loads live)
 //   GO2PI_DIAG_NOLOAD  — replace the weight loads by register arithmetic

@@ -53,6 +53,7 @@ constexpr int RES_GS = 4;    // GRU form: gate-fragment chunk slots per wave (I_
 constexpr int RES_PW = RES_WAVES - 1;
 
 typedef unsigned long long u64;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // GO2PI_DIAG_RESCLK builds (tools/res_timeline.py): wall-clock (100 MHz) stamps of
 // one request's path through workgroup 0 (slots 0..15) and workgroup 17 (16..31,
@@ -813,6 +814,14 @@ unsigned r1_shape(const DevProgram &p) {
   return fs;
 }
 
+// log2 of the group size of each layer of program p, packed as the kernel's GS
+unsigned r1_lgs(const DevProgram &p) {
+  unsigned gs = 0;
+  for (int l = 0; l < p.nl && l < R1_LMAX; ++l)
+    gs |= (unsigned)__builtin_ctz(r1_group(p.L[l].N_pad, l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS)) << (4 * l);
+  return gs;
+}
+
 bool resident1_fits(const DevProgram &p) {
   if (p.has_gru || p.nl < 1 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
   for (int l = 0; l < p.nl; ++l) {
@@ -821,7 +830,7 @@ bool resident1_fits(const DevProgram &p) {
     if (p.L[l].N_pad * G > thr) return false;
     if ((p.L[l].K_pad + 4 * G - 1) / (4 * G) > R1_FMAX) return false;
   }
-  return true;
+  return p.L[0].K_pad <= R1_THREADS;
 }
 
 // CTL: the controller tick (go2pi_controller_step at batch <= 8), as the multi-
@@ -833,7 +842,12 @@ bool resident1_fits(const DevProgram &p) {
 // FS: weight float4s per lane of each layer, packed as 4-bit fields (layer l in bits
 // 4l..4l+3), so a policy shape gets exactly the registers its layers need (the
 // shipped model: 4, 4, 4, 1); the generic instantiation holds R1_FMAX for every layer.
-template <int LMAX, int FMAX, bool CTL, unsigned FS = 0x4444u>
+// GS: log2 of each layer's group size, packed the same way (the shipped model: 3, 3,
+// 3, 5), or 0: computed at run time. At compile time every lane index is a shift and
+// every input offset an immediate: with 16 waves sharing 4 SIMDs a layer is VALU-issue
+// bound, and the run-time group size cost integer divisions per layer (measured 2.9K
+// cycles per 128 x 128 layer, 1.15K of them before the sums; profiles/r04_res_timeline.json).
+template <int LMAX, int FMAX, bool CTL, unsigned FS = 0x4444u, unsigned GS = 0u>
 __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevProgram *__restrict__ Pd,
                                                                       const u64 *req, u64 *actg, unsigned *err,
                                                                       unsigned *done, u64 idle_ticks,
@@ -888,13 +902,14 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
   // (layer dims -> group size -> addresses; activation kind; the epilogue) is an L2
   // round trip on the request's path. The empty asm makes each value opaque, so the
   // compiler keeps it (in an SGPR, or a VGPR lane when it spills) instead of reloading.
-  int lK[LMAX], lNp[LMAX], lact[LMAX];
+  int lK[LMAX], lNp[LMAX], lact[LMAX], lgr[LMAX];
   float lal[LMAX], lbe[LMAX];
 #pragma unroll
   for (int l = 0; l < LMAX; ++l) {
     const DevLayer &L = P.L[l < nl ? l : 0];
     lK[l] = r1_keep(L.K_pad);
     lNp[l] = r1_keep(L.N_pad);
+    lgr[l] = GS ? 0 : r1_keep(__builtin_ctz(r1_group(L.N_pad, l == nl - 1 ? R1_THREADS - 64 : R1_THREADS)));
     lact[l] = r1_keep(L.act);
     lal[l] = r1_keep(L.alpha);
     lbe[l] = r1_keep(L.beta);
@@ -962,44 +977,46 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     }
     // layer 0's input rows: the observation through the prologue, zeros past in_dim
     {
-      const int K0 = lK[0];
-      for (int i = tid; i < B * K0; i += R1_THREADS) {
-        const int b = i / K0, k = i - b * K0;
-        const float v = k < in_dim ? obsv[b * in_dim + k] : 0.f;
-        xa[b * S + k] = (k >= in_dim || pro_plain) ? v : prologue(P, v, k);
-      }
+      const int K0 = lK[0];  // (<= the threads: resident1_fits)
+      if (tid < K0)
+        for (int b = 0; b < B; ++b) {
+          const float v = tid < in_dim ? obsv[b * in_dim + tid] : 0.f;
+          xa[b * S + tid] = (tid >= in_dim || pro_plain) ? v : prologue(P, v, tid);
+        }
     }
     lds_barrier();
     RES_STAMP(1);
+    RES_CLOCK(13);
     float *X = xa, *Y = xb;
 #pragma unroll
     for (int l = 0; l < LMAX; ++l) {
       if (l < nl) {
         const bool lastl = l == nl - 1;
-        const int G = r1_group(lNp[l], lastl ? R1_THREADS - 64 : R1_THREADS), K = lK[l];
+        const int lg = GS ? (int)((GS >> (4 * l)) & 15u) : lgr[l], G = 1 << lg, K = lK[l];
         const int t = lastl ? tid - 64 : tid;
-        const int n = t / G, sl = t % G;
+        const int n = t >> lg, sl = t & (G - 1);
         const bool mine = t >= 0 && n < lNp[l];
+        const bool kfull = GS != 0u && 4 * G * (int)((FS >> (4 * l)) & 15u) <= K;  // no k past K_pad
         for (int b = 0; b < B; ++b) {
-          float a0 = 0.f, a1 = 0.f;
+          // two packed (v_pk_fma_f32) chains over the lane's float4s: f even / odd
+          f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
           if (mine) {
-            const float *xr = X + b * S;
+            const float *xr = X + b * S + 4 * sl;
 #pragma unroll
             for (int f = 0; f < FMAX; ++f) {
-              const int k = 4 * (sl + G * f);
-              if (f < (int)((FS >> (4 * l)) & 15u) && k < K) {
-                const float4 x = *reinterpret_cast<const float4 *>(xr + k);
-                float &a = (f & 1) ? a1 : a0;
-                a = fmaf(x.x, w[l][f].x, a);
-                a = fmaf(x.y, w[l][f].y, a);
-                a = fmaf(x.z, w[l][f].z, a);
-                a = fmaf(x.w, w[l][f].w, a);
+              if (f < (int)((FS >> (4 * l)) & 15u) && (kfull || 4 * (sl + G * f) < K)) {
+                const float4 x = *reinterpret_cast<const float4 *>(xr + 4 * G * f);
+                f32x2 &a = (f & 1) ? a1 : a0;
+                a = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{w[l][f].x, w[l][f].y}, a);
+                a = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{w[l][f].z, w[l][f].w}, a);
               }
             }
           }
+          if (l < 3 && b == 0) RES_CLOCK(16 + 3 * l);  // layer l: fma chains done (shader clock)
           // (lanes past the layer's outputs, and the final layer's wave 0, join the
           // group sums with zeros: the DPP tree runs on whole rows)
-          const float v = r1_group_sum(a0 + a1, G);
+          const float v = r1_group_sum((a0.x + a0.y) + (a1.x + a1.y), G);
+          if (l < 3 && b == 0) RES_CLOCK(17 + 3 * l);  // group sums done
           if (mine && sl == 0) {
             const float y = act_fn(lact[l], lal[l], lbe[l], v + bias[l]);
             if (!lastl) Y[b * S + n] = y;
@@ -1012,9 +1029,11 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
             }
           }
         }
+        if (l < 3) RES_CLOCK(18 + 3 * l);  // layer l's outputs stored (this wave's)
         if (!lastl) {
           lds_barrier();
           if (l < 6) RES_STAMP(2 + l);  // layer l's outputs in LDS
+          if (l < 3) RES_CLOCK(25 + l);  // (shader clock) past the layer's barrier
           float *t = X;
           X = Y;
           Y = t;
@@ -1063,9 +1082,9 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
   };
   // the shipped model's shape (98 -> 128^3 -> 12: 4, 4, 4, 1 float4s per lane) has its own
   // instantiation: the registers it leaves free keep the controller form out of scratch
-  if (p.nl == 4 && r1_shape(p) == 0x1444u)
-    return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true, 0x1444u>)
-               : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false, 0x1444u>);
+  if (p.nl == 4 && r1_shape(p) == 0x1444u && r1_lgs(p) == 0x5333u)
+    return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true, 0x1444u, 0x5333u>)
+               : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false, 0x1444u, 0x5333u>);
   return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true>) : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false>);
 }
 

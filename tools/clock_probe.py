@@ -87,6 +87,12 @@ def main():
         gru_sub = {"entry": float(np.median(st[:, 43] - st[:, 0])),
                    "contraction": float(np.median(st[:, 44] - st[:, 43])),
                    "epilogue": float(np.median(st[:, 45] - st[:, 44]))}
+    blocks = {}
+    if args.ctl and np.all(st[:, 56] > 0):  # the assembly's blocks (slots 50..56, thread 0) from slot 5
+        prev = st[:, 5]
+        for b in range(7):
+            blocks[f"block{b}"] = float(np.median(st[:, 50 + b] - prev))
+            prev = st[:, 50 + b]
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
         names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
@@ -107,7 +113,8 @@ def main():
            "wg_end_spread_us": float((st[:, 3].max() - st[:, 3].min()) / 100),
            "phase_cycles_median": phases,
            "layer1_wave_marks": waves_l1,  # [entry, contraction done, epilogue done, barrier] cycles
-           "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub, "gru_stage": gru_sub}
+           "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub, "gru_stage": gru_sub,
+           "ctl_assembly_blocks": blocks}
     print(json.dumps(out))
 
 

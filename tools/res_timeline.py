@@ -109,7 +109,25 @@ def one_workgroup(args, st, ts, np):
         med[names[s_]] = {"at_us": round(m, 3), "step_us": round(m - prev, 3)}
         prev = m
     gaps = (rows[1:, 0] - rows[:-1, 8]) * 10.0 / 1e3
+    # shader clock (s_memtime, slots 13..30) over the wall clock from seen (15) to answer (14)
+    dwall = (rows[:, 8] - rows[:, 0]) * 10e-9
+    ghz = (rows[:, 14] - rows[:, 15]) / np.maximum(dwall, 1e-9) / 1e9
+    cyc = {}
+    marks = [(13, "input staged")]
+    for l in range(3):
+        marks += [(16 + 3 * l, f"layer{l} fma done"), (17 + 3 * l, f"layer{l} group sums done"),
+                  (18 + 3 * l, f"layer{l} outputs stored"), (25 + l, f"layer{l} barrier passed")]
+    marks += [(14, "answer issued")]
+    prev = rows[:, 15]
+    for s_, nm in marks:
+        ok = rows[:, s_] > 0
+        if ok.sum() < len(rows) // 2:
+            continue
+        cyc[nm] = float(np.median((rows[ok, s_] - prev[ok])))
+        prev = np.where(ok, rows[:, s_], prev)
     out = {"model": args.model, "kernel": "policy_resident1_kernel (one workgroup)",
+           "shader_clock_ghz_median": round(float(np.median(ghz)), 3),
+           "wave0_cycles_since_previous_mark": cyc,
            "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2], "host_p99_us": ts[int(len(ts) * 0.99)],
            "median_from_request_seen": med,
            "median_answer_to_next_seen_us": round(float(np.median(gaps)), 3)}
