@@ -141,7 +141,7 @@ __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
 
 // One history block BK of the new observation rows r < nrows, on one wave's
 // lanes: straight-line code per block (BK is a template parameter).
-template <int BK, bool TILE>
+template <int BK, bool TILE, int UNR = 2>
 __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
                                                float *dst_, int ds, float *raw_, int lane, int stride = 64) {
   // the LDS image, the destination tile and the caller's rows never overlap: without
@@ -157,7 +157,7 @@ __device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds
   const int H = q.hist, in_dim = q.in_dim;
   const int W = H * d, s0 = H * cum, sh = (H - 1) * d;
   const float rW = 1.f / (float)W;
-#pragma unroll 2
+#pragma unroll UNR
   for (int e = lane; e < nrows * W; e += stride) {
     // r = e / W exactly: (e + 0.5) / W is >= 0.5 / W away from an integer and the
     // float product's error is far below that for these sizes (W <= 49 * 16)
@@ -240,23 +240,24 @@ __device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L
 // (thread t, stride nt), the blocks one after another: at 4 waves per workgroup
 // the one-job-per-wave split left each wave two whole blocks in series
 // (measured 9.6K cycles for the tile, against ~4K at 8 waves).
-template <bool TILE>
+// UNR: elements per thread in flight (1 where registers are scarce: the resident kernels)
+template <bool TILE, int UNR = 2>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
   // (GO2PI_DIAG_CLOCK: thread 0's time after each block, slots 50 + block)
-  ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<0, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 50);
-  ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<1, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 51);
-  ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<2, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 52);
-  ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<3, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 53);
-  ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<4, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 54);
-  ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<5, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 55);
-  ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_block_pass<6, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 56);
   if constexpr (TILE) {  // padding columns [in_dim, in_pad) and rows [nrows, 16)
     const int in_dim = q.in_dim, pw = q.in_pad - in_dim;

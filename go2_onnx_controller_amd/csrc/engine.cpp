@@ -149,6 +149,7 @@ struct go2pi_engine {
   unsigned long long *d_hgran = nullptr;  // GRU form: [2][SMALL_MAXB][H] hidden-row granules (two buffers)
   bool resident_ctl = false;  // the live kernel is the controller-tick form
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
+  bool resident1_ctl = false; // controller form in one workgroup (512 threads)
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
   unsigned long long *d_mirror = nullptr;                 // device copy of the request (workgroup 0 -> the rest)
@@ -268,7 +269,7 @@ struct go2pi_engine {
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
     std::memset(h_actg, 0, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)model.out_dim);
-    if (resident1)
+    if (ctl ? resident1_ctl : resident1)
       hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, ctl,
                                         stream),
                 "resident launch (one workgroup)");
@@ -870,7 +871,8 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   // a dense policy whose weights fit one CU's registers is served by the single-
   // workgroup resident kernel (no inter-workgroup hop per layer; GO2PI_RES_MULTI=1:
   // the multi-workgroup form, A/B diagnostics)
-  e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p) && !std::getenv("GO2PI_RES_MULTI");
+  e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, false) && !std::getenv("GO2PI_RES_MULTI");
+  e.resident1_ctl = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, true) && !std::getenv("GO2PI_RES_MULTI");
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");

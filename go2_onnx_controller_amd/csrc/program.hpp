@@ -230,7 +230,7 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
 // The single-workgroup resident form (resident.hip policy_resident1_kernel, r04):
 // dense policies of <= 4 layers whose weights fit one CU's registers, at most 16
 // outputs. Same request / answer / leave protocol as launch_resident.
-bool resident1_fits(const DevProgram &p);
+bool resident1_fits(const DevProgram &p, bool ctl);  // ctl: the controller form (512 threads)
 // ctl non-null: the controller-tick form (launch_resident's ctl semantics).
 int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,

@@ -121,9 +121,12 @@ template <int SCOPE, int NP = RES_POLL>
 // yield (workgroup 0 only, else null): the device's batched-launch counter (every
 // batched kernel adds 1 at its start); a change since y0 means a batched kernel
 // wants the CUs this kernel holds: leave (the next request relaunches).
+// row1 (optional): where a one-row request's values go instead of obsv (the single-
+// workgroup kernel's layer-0 input row: no staging copy when no prologue applies)
 __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned last, u64 idle_ticks, float *obsv,
                                              unsigned *err, int lane, int &leave, unsigned &e, int &B,
-                                             unsigned &word, const unsigned *yield = nullptr, unsigned y0 = 0) {
+                                             unsigned &word, const unsigned *yield = nullptr, unsigned y0 = 0,
+                                             float *row1 = nullptr) {
   u64 *qm = const_cast<u64 *>(q);
   const u64 t0 = wall_clock64();
   const int npoll = min(1 + in_dim, 64 * NP);
@@ -150,12 +153,13 @@ __device__ __forceinline__ void wait_request(const u64 *q, int in_dim, unsigned 
       const int n = B * in_dim;  // observation granules q[1 .. n]
       if (1 + n <= npoll) {
         bool ok = true;
+        float *dst = (row1 && B == 1) ? row1 : obsv;
 #pragma unroll
         for (int u = 0; u < NP; ++u) {
           const int i = u * 64 + lane;
           if (u * 64 < npoll && i >= 1 && i <= n) {
             ok &= (unsigned)(v[u] >> 32) == e;
-            obsv[i - 1] = __uint_as_float((unsigned)v[u]);
+            dst[i - 1] = __uint_as_float((unsigned)v[u]);
           }
         }
         if (__all(ok)) return;
@@ -751,7 +755,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
 //  * 16 waves; dense layer l gives each output n a group of G_l adjacent lanes of
 //    one wave (G_l = the largest power of two with N_pad * G_l <= the threads, at
 //    most 64), lane s of the group owns the input float4s k4 = s + G_l * f, f <
-//    F_l <= R1_FMAX. Those F_l weight float4s sit in the lane's registers for the
+//    F_l <= r1_fmax(threads). Those F_l weight float4s sit in the lane's registers for the
 //    kernel's life (loaded once from the packed fragments, program.hpp);
 //  * per request and row: F_l broadcast ds_read_b128 of the input row, 4 F_l fmas
 //    in two chains, the group's sum by DPP row permutes (quad xor 1, quad xor 2,
@@ -767,13 +771,16 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
 // Summation order: per output, two fma chains over its lane's k (f even / odd),
 // then the fixed DPP tree over the group: deterministic, not bit-identical to the
 // launch path's MFMA order (both within the 1e-5 contract of the fp64 oracle).
-constexpr int R1_THREADS = 1024;
 constexpr int R1_LMAX = 4;  // dense layers
-constexpr int R1_FMAX = 4;  // weight float4s per lane per layer (16 floats)
+// threads: 1024 (16 waves, 128 registers each) for act(); the controller form runs 512
+// (8 waves, 256 registers each: the assembly's registers beside the weights spilled to
+// scratch at 1024), twice the weight float4s per lane
+__host__ __device__ constexpr int r1_fmax(int nt) { return nt >= 1024 ? 4 : 8; }
 
-// lanes per output for a layer of n_pad outputs over `threads` lanes
+// lanes per output for a layer of n_pad outputs over `threads` lanes (at most 16: a
+// group's sum then stays within a DPP row, no cross-row permute through LDS)
 __host__ __device__ constexpr int r1_group(int n_pad, int threads) {
-  int g = 64;
+  int g = 16;
   while (g > 1 && n_pad * g > threads) g >>= 1;
   return g;
 }
@@ -804,33 +811,41 @@ __device__ __forceinline__ float r1_group_sum(float v, int G) {
 }
 
 // the per-layer float4 counts of program p, packed as the kernel's FS
-unsigned r1_shape(const DevProgram &p) {
+unsigned r1_shape(const DevProgram &p, int nt) {
   unsigned fs = 0;
   for (int l = 0; l < p.nl && l < R1_LMAX; ++l) {
-    const int thr = l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS;
+    const int thr = l == p.nl - 1 ? nt - 64 : nt;
     const int G = r1_group(p.L[l].N_pad, thr);
     fs |= (unsigned)((p.L[l].K_pad + 4 * G - 1) / (4 * G)) << (4 * l);
   }
   return fs;
 }
 
+// the activation kind of each layer of program p, packed as the kernel's AS
+unsigned r1_acts(const DevProgram &p) {
+  unsigned as = 0;
+  for (int l = 0; l < p.nl && l < R1_LMAX; ++l) as |= (unsigned)(p.L[l].act & 15) << (4 * l);
+  return as;
+}
+
 // log2 of the group size of each layer of program p, packed as the kernel's GS
-unsigned r1_lgs(const DevProgram &p) {
+unsigned r1_lgs(const DevProgram &p, int nt) {
   unsigned gs = 0;
   for (int l = 0; l < p.nl && l < R1_LMAX; ++l)
-    gs |= (unsigned)__builtin_ctz(r1_group(p.L[l].N_pad, l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS)) << (4 * l);
+    gs |= (unsigned)__builtin_ctz(r1_group(p.L[l].N_pad, l == p.nl - 1 ? nt - 64 : nt)) << (4 * l);
   return gs;
 }
 
-bool resident1_fits(const DevProgram &p) {
+bool resident1_fits(const DevProgram &p, bool ctl) {
+  const int nt = ctl ? 512 : 1024;
   if (p.has_gru || p.nl < 1 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
   for (int l = 0; l < p.nl; ++l) {
-    const int thr = l == p.nl - 1 ? R1_THREADS - 64 : R1_THREADS;
+    const int thr = l == p.nl - 1 ? nt - 64 : nt;
     const int G = r1_group(p.L[l].N_pad, thr);
     if (p.L[l].N_pad * G > thr) return false;
-    if ((p.L[l].K_pad + 4 * G - 1) / (4 * G) > R1_FMAX) return false;
+    if ((p.L[l].K_pad + 4 * G - 1) / (4 * G) > r1_fmax(nt)) return false;
   }
-  return p.L[0].K_pad <= R1_THREADS;
+  return p.L[0].K_pad <= nt;
 }
 
 // CTL: the controller tick (go2pi_controller_step at batch <= 8), as the multi-
@@ -841,21 +856,24 @@ bool resident1_fits(const DevProgram &p) {
 // then the done word.
 // FS: weight float4s per lane of each layer, packed as 4-bit fields (layer l in bits
 // 4l..4l+3), so a policy shape gets exactly the registers its layers need (the
-// shipped model: 4, 4, 4, 1); the generic instantiation holds R1_FMAX for every layer.
+// shipped model: 4, 4, 4, 1); the generic instantiation holds FMAX for every layer.
 // GS: log2 of each layer's group size, packed the same way (the shipped model: 3, 3,
 // 3, 5), or 0: computed at run time. At compile time every lane index is a shift and
 // every input offset an immediate: with 16 waves sharing 4 SIMDs a layer is VALU-issue
 // bound, and the run-time group size cost integer divisions per layer (measured 2.9K
 // cycles per 128 x 128 layer, 1.15K of them before the sums; profiles/r04_res_timeline.json).
-template <int LMAX, int FMAX, bool CTL, unsigned FS = 0x4444u, unsigned GS = 0u>
-__global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevProgram *__restrict__ Pd,
+// AS: each layer's activation kind packed the same way (the shipped model: Elu, Elu,
+// Elu, none = 0x0111), or 0xFFFFFFFF: read at run time.
+template <int NT, int LMAX, int FMAX, bool CTL, unsigned FS = 0x4444u, unsigned GS = 0u, unsigned AS = 0xFFFFFFFFu>
+__global__ __launch_bounds__(NT) void policy_resident1_kernel(const DevProgram *__restrict__ Pd,
                                                                       const u64 *req, u64 *actg, unsigned *err,
                                                                       unsigned *done, u64 idle_ticks,
                                                                       const unsigned *yield, DevCtl C) {
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
   const int S = P.lds_stride;
-  float *xa = reinterpret_cast<float *>(lds4);           // [8][S] layer input rows
+  float *x0 = reinterpret_cast<float *>(lds4);           // [8][S] layer 0's input rows (zero past in_dim)
+  float *xa = x0 + GO2PI_SMALL_MAXB * S;                 // [8][S] hidden layers' rows (ping-pong)
   float *xb = xa + GO2PI_SMALL_MAXB * S;                 // [8][S]
   int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch, [3] word
   float *obsv = reinterpret_cast<float *>(st + 4);       // [8][in_dim] the request's observation
@@ -881,7 +899,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     if (l < nl && l < LMAX) {
       const DevLayer &L = P.L[l];
       const bool lastl = l == nl - 1;
-      const int G = r1_group(L.N_pad, lastl ? R1_THREADS - 64 : R1_THREADS);
+      const int G = r1_group(L.N_pad, lastl ? NT - 64 : NT);
       const int t = lastl ? tid - 64 : tid;  // the final layer skips wave 0 (the poller)
       const int n = t / G, sl = t % G;
       if (t >= 0 && n < L.N_pad) {
@@ -909,7 +927,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     const DevLayer &L = P.L[l < nl ? l : 0];
     lK[l] = r1_keep(L.K_pad);
     lNp[l] = r1_keep(L.N_pad);
-    lgr[l] = GS ? 0 : r1_keep(__builtin_ctz(r1_group(L.N_pad, l == nl - 1 ? R1_THREADS - 64 : R1_THREADS)));
+    lgr[l] = GS ? 0 : r1_keep(__builtin_ctz(r1_group(L.N_pad, l == nl - 1 ? NT - 64 : NT)));
     lact[l] = r1_keep(L.act);
     lal[l] = r1_keep(L.alpha);
     lbe[l] = r1_keep(L.beta);
@@ -921,6 +939,10 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
     if (post_tanh) v = tanhf(v);
     return clip_nan(v, clo, chi) * pscale;
   };
+  // layer 0's input rows start (and, past in_dim, stay) zero
+  for (int i = tid; i < GO2PI_SMALL_MAXB * S; i += NT) x0[i] = 0.f;
+  // a one-row act() request with no prologue lands in x0 straight from the poll
+  const bool direct = !CTL && pro_plain && 1 + in_dim <= 64 * RES_POLL;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights are in registers before the first wait
   const unsigned y0 = yield ? __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)
@@ -936,7 +958,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
                                                    leave, e, B, word, yield, y0);
       else
         wait_request<__HIP_MEMORY_SCOPE_SYSTEM>(req, in_dim, last, idle_ticks, obsv, err, lane, leave, e, B, word,
-                                                yield, y0);
+                                                yield, y0, direct ? x0 : nullptr);
       RES_STAMP(0);
       RES_CLOCK(15);
       if (lane == 0) {
@@ -959,14 +981,14 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
       // rows) into the assembly's LDS image, then the observation assembled into obsv
       const bool joy = (word & GO2PI_RES_JOY) != 0u;
       const int o_jy = B * GO2PI_CTL_STATE_DIM, o_obs = o_jy + B * GO2PI_CTL_JOY_DIM, o_act = o_obs + B * in_dim;
-      for (int i = tid; i < o_jy; i += R1_THREADS) CL.st[i] = craw[i];
-      for (int i = tid; i < B * GO2PI_CTL_JOY_DIM; i += R1_THREADS) CL.jy[i] = craw[o_jy + i];
-      for (int i = tid; i < B * in_dim; i += R1_THREADS) CL.obs[i] = craw[o_obs + i];
-      for (int i = tid; i < B * GO2PI_CTL_DOF; i += R1_THREADS) CL.act[i] = craw[o_act + i];
+      for (int i = tid; i < o_jy; i += NT) CL.st[i] = craw[i];
+      for (int i = tid; i < B * GO2PI_CTL_JOY_DIM; i += NT) CL.jy[i] = craw[o_jy + i];
+      for (int i = tid; i < B * in_dim; i += NT) CL.obs[i] = craw[o_obs + i];
+      for (int i = tid; i < B * GO2PI_CTL_DOF; i += NT) CL.act[i] = craw[o_act + i];
       if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
       if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
       __syncthreads();
-      ctl_assemble_flat<false>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, R1_THREADS);
+      ctl_assemble_flat<false, 1>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, NT);
       DevCtl c = C;
       if (!joy) c.joy = nullptr;
       if (!(word & GO2PI_RES_QDES)) c.q_des = nullptr;
@@ -975,19 +997,19 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
       cv = ctl_view(c, CL, 0);
       lds_barrier();
     }
-    // layer 0's input rows: the observation through the prologue, zeros past in_dim
-    {
-      const int K0 = lK[0];  // (<= the threads: resident1_fits)
-      if (tid < K0)
+    // layer 0's input rows: the observation through the prologue (x0 past in_dim stays zero),
+    // unless the poll wrote the one row there itself
+    if (!(direct && B == 1)) {
+      if (tid < in_dim)
         for (int b = 0; b < B; ++b) {
-          const float v = tid < in_dim ? obsv[b * in_dim + tid] : 0.f;
-          xa[b * S + tid] = (tid >= in_dim || pro_plain) ? v : prologue(P, v, tid);
+          const float v = obsv[b * in_dim + tid];
+          x0[b * S + tid] = pro_plain ? v : prologue(P, v, tid);
         }
+      lds_barrier();
     }
-    lds_barrier();
     RES_STAMP(1);
     RES_CLOCK(13);
-    float *X = xa, *Y = xb;
+    float *X = x0, *Y = xa;
 #pragma unroll
     for (int l = 0; l < LMAX; ++l) {
       if (l < nl) {
@@ -1018,7 +1040,9 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
           const float v = r1_group_sum((a0.x + a0.y) + (a1.x + a1.y), G);
           if (l < 3 && b == 0) RES_CLOCK(17 + 3 * l);  // group sums done
           if (mine && sl == 0) {
-            const float y = act_fn(lact[l], lal[l], lbe[l], v + bias[l]);
+            // (AS: the kind is a constant once the layer loop is unrolled, and the switch folds)
+            const int A = AS != 0xFFFFFFFFu ? (int)((AS >> (4 * l)) & 15u) : lact[l];
+            const float y = act_fn(A, lal[l], lbe[l], v + bias[l]);
             if (!lastl) Y[b * S + n] = y;
             else if (n < nout) {
               if constexpr (CTL)
@@ -1034,16 +1058,15 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
           lds_barrier();
           if (l < 6) RES_STAMP(2 + l);  // layer l's outputs in LDS
           if (l < 3) RES_CLOCK(25 + l);  // (shader clock) past the layer's barrier
-          float *t = X;
           X = Y;
-          Y = t;
+          Y = Y == xa ? xb : xa;
         }
       }
     }
     RES_STAMP(8);  // answer issued (this wave's)
     RES_CLOCK(14);
     if constexpr (CTL) {  // the new observation rows and NaN flags, then the done word
-      for (int i = tid; i < B * in_dim; i += R1_THREADS) C.obs[i] = obsv[i];
+      for (int i = tid; i < B * in_dim; i += NT) C.obs[i] = obsv[i];
       if ((word & GO2PI_RES_STATUS) && tid < B) C.status[tid] = CL.nanf[tid];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1059,7 +1082,7 @@ __global__ __launch_bounds__(R1_THREADS) void policy_resident1_kernel(const DevP
 }
 
 size_t resident1_lds_bytes(const DevProgram &p, bool ctl) {
-  size_t f = 2 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + ((size_t)GO2PI_SMALL_MAXB * p.in_dim + 3) / 4 * 4;
+  size_t f = 3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + ((size_t)GO2PI_SMALL_MAXB * p.in_dim + 3) / 4 * 4;
   if (ctl) f += (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
   return sizeof(float) * f;
 }
@@ -1067,25 +1090,31 @@ size_t resident1_lds_bytes(const DevProgram &p, bool ctl) {
 int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
                      const unsigned *yield, const DevCtl *ctl, void *stream) {
-  if (!resident1_fits(p)) return (int)hipErrorInvalidValue;
+  if (!resident1_fits(p, ctl != nullptr)) return (int)hipErrorInvalidValue;
   const size_t lds = resident1_lds_bytes(p, ctl != nullptr);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  auto go = [&](auto kern) {
+  auto go = [&](auto kern, int nt) {
     if (lds > 64 * 1024) {
       const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (a != hipSuccess) return (int)a;
     }
-    hipLaunchKernelGGL(kern, dim3(1), dim3(R1_THREADS), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
+    hipLaunchKernelGGL(kern, dim3(1), dim3(nt), lds, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
                        err, done, idle_ticks, yield, ctl ? *ctl : DevCtl{});
     return (int)hipGetLastError();
   };
   // the shipped model's shape (98 -> 128^3 -> 12: 4, 4, 4, 1 float4s per lane) has its own
   // instantiation: the registers it leaves free keep the controller form out of scratch
-  if (p.nl == 4 && r1_shape(p) == 0x1444u && r1_lgs(p) == 0x5333u)
-    return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true, 0x1444u, 0x5333u>)
-               : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false, 0x1444u, 0x5333u>);
-  return ctl ? go(policy_resident1_kernel<R1_LMAX, R1_FMAX, true>) : go(policy_resident1_kernel<R1_LMAX, R1_FMAX, false>);
+  // (Elu alpha 1 on the hidden layers, no activation on the head: the exported policy's)
+  const bool elu1 = r1_acts(p) == 0x0111u && p.L[0].alpha == 1.f && p.L[1].alpha == 1.f && p.L[2].alpha == 1.f;
+  if (ctl) {
+    if (p.nl == 4 && elu1 && r1_shape(p, 512) == 0x2887u && r1_lgs(p, 512) == 0x4222u)
+      return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x2887u, 0x4222u, 0x0111u>, 512);
+    return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x8888u>, 512);
+  }
+  if (p.nl == 4 && elu1 && r1_shape(p, 1024) == 0x2444u && r1_lgs(p, 1024) == 0x4333u)
+    return go(policy_resident1_kernel<1024, R1_LMAX, 4, false, 0x2444u, 0x4333u, 0x0111u>, 1024);
+  return go(policy_resident1_kernel<1024, R1_LMAX, 4, false>, 1024);
 }
 
 int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
