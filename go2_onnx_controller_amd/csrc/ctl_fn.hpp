@@ -139,138 +139,115 @@ __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
               pro_of(P)};
 }
 
-// One history block BK of the new observation rows r < nrows, on one wave's
-// lanes: straight-line code per block (BK is a template parameter).
-template <int BK, bool TILE, int UNR = 2>
-__device__ __forceinline__ void ctl_block_pass(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
-                                               float *dst_, int ds, float *raw_, int lane, int stride = 64) {
-  // the LDS image, the destination tile and the caller's rows never overlap: without
+// Block b of the 49 values a tick appends per robot (controller.cpp:210-212):
+// 0 gravity_b 3, 1 base_ang_vel 3, 2 vel_cmd 3, 3 q - q0 12, 4 dq 12, 5 action 12,
+// 6 contacts 4. cum: the block's first value among the 49; d: its width. In the
+// observation row block b spans [H * cum, H * (cum + d)), the newest d values last.
+__device__ __forceinline__ int ctl_cum(int b) { return b < 3 ? 3 * b : (b < 6 ? 9 + 12 * (b - 3) : 45); }
+__device__ __forceinline__ int ctl_width(int b) { return b < 3 ? 3 : (b < 6 ? 12 : 4); }
+
+// The appended values of rows r < nrows: element (i, r) of the 49 x rows grid
+// (row index fastest, so a wave's lanes share one or two blocks' code). Per
+// element: the raw value goes to raw[r * in_dim + k] (the tile's global obs rows;
+// may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k]. NaN among the
+// appended values of blocks 0-5 — where the reference's populate_buffer check
+// exit(1)s (controller.hpp:57-64) — sets nanf[r].
+template <bool TILE>
+__device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool joy, int nrows, float *__restrict__ dst,
+                                           int ds, float *__restrict__ raw, int tid, int nt) {
+  // the LDS image, the destination and the caller's rows never overlap: without
   // __restrict__ every element's reads waited behind the previous element's stores
   const float *__restrict__ obs_l = L.obs;
   const float *__restrict__ st_l = L.st;
   const float *__restrict__ jy_l = L.jy;
   const float *__restrict__ act_l = L.act;
-  float *__restrict__ dst = dst_;
-  float *__restrict__ raw = raw_;
-  constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
-  constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
   const int H = q.hist, in_dim = q.in_dim;
-  const int W = H * d, s0 = H * cum, sh = (H - 1) * d;
-  const float rW = 1.f / (float)W;
-#pragma unroll UNR
-  for (int e = lane; e < nrows * W; e += stride) {
-    // r = e / W exactly: (e + 0.5) / W is >= 0.5 / W away from an integer and the
-    // float product's error is far below that for these sizes (W <= 49 * 16)
-    const int r = (int)(((float)e + 0.5f) * rW);
-    const int j = e - r * W, k = s0 + j;
-    const float *orow = obs_l + r * in_dim;
+  const int lg = nrows <= 1 ? 0 : 32 - __builtin_clz(nrows - 1);
+  for (int e = tid; e < (GO2PI_CTL_STEP_DIM << lg); e += nt) {
+    const int r = e & ((1 << lg) - 1), i = e >> lg;
+    if (r >= nrows) continue;
+    const int b = (i >= 3) + (i >= 6) + (i >= 9) + (i >= 21) + (i >= 33) + (i >= 45);
+    const int cum = ctl_cum(b), d = ctl_width(b), c = i - cum;
+    const int k = H * cum + (H - 1) * d + c;
+    const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
     float v;
-    if (j < sh) {
-      v = orow[k + d];  // std::shift_left by d
-    } else {
-      const int i = j - sh;
-      const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
-      if constexpr (BK == 0) {
-        v = ctl_gravity(st, q.g0, q.g1, q.g2, i);
-      } else if constexpr (BK == 1) {
-        v = st[4 + i];  // imu gyroscope (controller.hpp:105-109)
-      } else if constexpr (BK == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
-        const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
-        if (!joy || jy[0] == 0.f) v = orow[k];  // the previous tick's vel_cmd_
-        else if (i == 0) v = jy[2];             // axes[1]
-        else if (i == 2) v = jy[3] * jy[2];     // axes[3] * axes[1]
-        else {                                  // pow(axes[0], 2) * sign * 0.8 in double
-          const double a0 = jy[1];
-          v = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
-        }
-      } else if constexpr (BK == 3) {
-        v = (float)((double)st[7 + i] - L.q0[i]);  // q_[i] -= q0_[i] (double q0_)
-      } else if constexpr (BK == 4) {
-        v = st[19 + i];
-      } else if constexpr (BK == 5) {
-        v = act_l[r * GO2PI_CTL_DOF + i];  // action_ before act()
-      } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
-        v = st[31 + (i ^ 1)] >= q.thr ? 1.f : 0.f;
+    if (b == 0) {
+      v = ctl_gravity(st, q.g0, q.g1, q.g2, c);
+    } else if (b == 1) {
+      v = st[4 + c];  // imu gyroscope (controller.hpp:105-109)
+    } else if (b == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
+      const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
+      if (!joy || jy[0] == 0.f) v = obs_l[r * in_dim + k];  // the previous tick's vel_cmd_
+      else if (c == 0) v = jy[2];                           // axes[1]
+      else if (c == 2) v = jy[3] * jy[2];                   // axes[3] * axes[1]
+      else {                                                // pow(axes[0], 2) * sign * 0.8 in double
+        const double a0 = jy[1];
+        v = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
       }
-      if (BK < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
+    } else if (b == 3) {
+      v = (float)((double)st[7 + c] - L.q0[c]);  // q_[i] -= q0_[i] (double q0_)
+    } else if (b == 4) {
+      v = st[19 + c];
+    } else if (b == 5) {
+      v = act_l[r * GO2PI_CTL_DOF + c];  // action_ before act()
+    } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
+      v = st[31 + (c ^ 1)] >= q.thr ? 1.f : 0.f;
     }
+    if (b < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
     if (raw) raw[r * in_dim + k] = v;
     dst[r * ds + k] = TILE ? prologue(q.pro, v, k) : v;
   }
 }
 
-// Assemble this tick's observation rows r < nrows from the LDS image: one job
-// per history block spread over the waves (each wave runs one block's
-// straight-line code), plus — TILE: dst is the batched kernel's LDS tile — a
-// job zeroing its padding columns [in_dim, in_pad) and rows [nrows, 16).
-// Per element: the raw value goes to raw[r * in_dim + k] (the tile's global
-// obs rows; may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k].
-// NaN among the appended values of blocks 0-5 — where the reference's
-// populate_buffer check exit(1)s (controller.hpp:57-64) — sets nanf[r].
-// Needs the image complete (barrier).
-template <bool TILE>
-__device__ __forceinline__ void ctl_assemble(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy, int nrows,
-                                             float *dst, int ds, float *raw, int wave, int lane, int nw) {
-  for (int job = wave; job < 8; job += nw) {
-    switch (job) {
-      case 0: ctl_block_pass<0, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 1: ctl_block_pass<1, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 2: ctl_block_pass<2, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 3: ctl_block_pass<3, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 4: ctl_block_pass<4, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 5: ctl_block_pass<5, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      case 6: ctl_block_pass<6, TILE>(P, L, q, joy, nrows, dst, ds, raw, lane); break;
-      default:
-        if constexpr (TILE) {  // padding
-          const int in_dim = q.in_dim, pw = q.in_pad - in_dim;
-          const float rp = 1.f / (float)pw;
-          for (int e = lane; e < nrows * pw; e += 64) {
-            const int r = (int)(((float)e + 0.5f) * rp);
-            dst[r * ds + in_dim + (e - r * pw)] = 0.f;
-          }
-          for (int r = nrows; r < GO2PI_TILE_ROWS; ++r)
-            for (int k = lane; k < q.in_pad; k += 64) dst[r * ds + k] = 0.f;
-        }
-        break;
+// The shifted values (std::shift_left by d, controller.hpp:45-52): column k of
+// every row r < nrows takes the image's column k + d. One column per thread, its
+// block, shift and prologue constants worked out once, then UNR rows' loads in
+// flight at a time. TILE: dst is the batched kernel's LDS tile — its padding
+// columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too.
+template <bool TILE, int UNR>
+__device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrows, float *__restrict__ dst, int ds,
+                                          float *__restrict__ raw, int tid, int nt) {
+  const float *__restrict__ obs_l = L.obs;
+  const int H = q.hist, in_dim = q.in_dim, kend = TILE ? q.in_pad : in_dim;
+  for (int k = tid; k < kend; k += nt) {
+    if (k >= in_dim) {
+      for (int r = 0; r < nrows; ++r) dst[r * ds + k] = 0.f;
+      continue;
+    }
+    const int b = (k >= 3 * H) + (k >= 6 * H) + (k >= 9 * H) + (k >= 21 * H) + (k >= 33 * H) + (k >= 45 * H);
+    const int cum = ctl_cum(b), d = ctl_width(b);
+    if (k - H * cum >= (H - 1) * d) continue;  // an appended column (ctl_append)
+    const ProK pk = pro_k(q.pro, k);
+#pragma unroll UNR
+    for (int r = 0; r < nrows; ++r) {
+      const float v = obs_l[r * in_dim + k + d];
+      if (raw) raw[r * in_dim + k] = v;
+      dst[r * ds + k] = TILE ? prologue(q.pro, pk, v) : v;
     }
   }
-}
-
-// The same assembly with every block spread over ALL the workgroup's threads
-// (thread t, stride nt), the blocks one after another: at 4 waves per workgroup
-// the one-job-per-wave split left each wave two whole blocks in series
-// (measured 9.6K cycles for the tile, against ~4K at 8 waves).
-// UNR: elements per thread in flight (1 where registers are scarce: the resident kernels)
-template <bool TILE, int UNR = 2>
-__device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
-                                                  int nrows, float *dst, int ds, float *raw, int tid, int nt) {
-  // (GO2PI_DIAG_CLOCK: thread 0's time after each block, slots 50 + block)
-  ctl_block_pass<0, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 50);
-  ctl_block_pass<1, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 51);
-  ctl_block_pass<2, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 52);
-  ctl_block_pass<3, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 53);
-  ctl_block_pass<4, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 54);
-  ctl_block_pass<5, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 55);
-  ctl_block_pass<6, TILE, UNR>(P, L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 56);
-  if constexpr (TILE) {  // padding columns [in_dim, in_pad) and rows [nrows, 16)
-    const int in_dim = q.in_dim, pw = q.in_pad - in_dim;
-    const float rp = 1.f / (float)pw;
-    for (int e = tid; e < nrows * pw; e += nt) {
-      const int r = (int)(((float)e + 0.5f) * rp);
-      dst[r * ds + in_dim + (e - r * pw)] = 0.f;
-    }
+  if constexpr (TILE)
     for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * q.in_pad; e += nt) {
       const int r = nrows + e / q.in_pad;
       dst[r * ds + (e - (r - nrows) * q.in_pad)] = 0.f;
     }
-  }
+}
+
+// Assemble this tick's observation rows r < nrows from the LDS image (needs the
+// image complete: barrier) over all nt threads of the workgroup: the appended
+// values (ctl_append) and the shifted ones (ctl_shift) go to disjoint columns, so
+// the two passes need no barrier between them. (The earlier form ran the seven
+// history blocks one after another, each element deriving its row, block and
+// source by division: ~10K cycles per 16-robot tile at 4 waves.)
+// UNR: rows in flight per thread in the shift pass (fewer where registers are
+// scarce: the resident kernels).
+template <bool TILE, int UNR = 8>
+__device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
+                                                  int nrows, float *dst, int ds, float *raw, int tid, int nt) {
+  // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
+  ctl_append<TILE>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 50);
+  ctl_shift<TILE, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 51);
 }
 
 // What the final layer's store needs (controller tick), by value: the call's

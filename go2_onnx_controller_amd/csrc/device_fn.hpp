@@ -141,4 +141,23 @@ __device__ __forceinline__ float prologue(const Pro &q, float v, int k) {
 
 __device__ __forceinline__ float prologue(const DevProgram &P, float v, int k) { return prologue(pro_of(P), v, k); }
 
+// One column's prologue constants, read once for a column applied to many rows
+// (the identity values where an op is absent: never applied, q's flags decide).
+struct ProK {
+  float sub, div, mul;
+};
+
+__device__ __forceinline__ ProK pro_k(const Pro &q, int k) {
+  return ProK{q.sub ? q.sub[q.sub_b ? 0 : k] : 0.f, q.div ? q.div[q.div_b ? 0 : k] : 1.f,
+              q.mul ? q.mul[q.mul_b ? 0 : k] : 1.f};
+}
+
+__device__ __forceinline__ float prologue(const Pro &q, const ProK &c, float v) {
+  if (q.sub) v -= c.sub;
+  if (q.div) v /= c.div;
+  if (q.mul) v *= c.mul;
+  if (q.clip) v = clip_nan(v, q.lo, q.hi);
+  return v;
+}
+
 }  // namespace go2pi

@@ -1177,9 +1177,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     // published to the caller's rows, and an LDS-only barrier hands X0 over
     ctl_here = step == 0 && !P.has_gru;
     if (ctl_here) {
+      const CtlQ cq = ctl_q(P, ctl);  // (its scalar loads land behind the barrier's wait)
       wg_barrier_vm<RD * TPW>();
       GO2PI_STAMP(P, threadIdx.x == 0, 5);
-      ctl_assemble_flat<true>(P, CL, ctl_q(P, ctl), ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
+      ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
                               ctl.obs + (size_t)row0 * P.in_dim, threadIdx.x, 256);
       lds_barrier();
     }
@@ -1500,12 +1501,8 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   auto stage_obs = [&](int step) {
     if constexpr (CTL) {  // this tile's rows of ctl.obs are read only from the LDS image: publish in place
       if (ctl_late) return;  // (w4_step)
-      if constexpr (NW == 4)
-        ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
-                                ctl.obs + (size_t)row0 * P.in_dim, tid, NT);
-      else
-        ctl_assemble<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
-                           ctl.obs + (size_t)row0 * P.in_dim, wave, lane, NW);
+      ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), bufA, S,
+                              ctl.obs + (size_t)row0 * P.in_dim, tid, NT);
     } else if (W4T > 0 && glds_obs) {
       // pipeline: wave w stages rows w, w + 4, w + 8, w + 12 in whole 64-column
       // chunks (in_pad is a GRU's input width, not always a multiple of 64);

@@ -988,7 +988,7 @@ __global__ __launch_bounds__(NT) void policy_resident1_kernel(const DevProgram *
       if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
       if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
       __syncthreads();
-      ctl_assemble_flat<false, 1>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, NT);
+      ctl_assemble_flat<false, 2>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, NT);
       DevCtl c = C;
       if (!joy) c.joy = nullptr;
       if (!(word & GO2PI_RES_QDES)) c.q_des = nullptr;

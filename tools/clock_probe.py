@@ -88,10 +88,10 @@ def main():
                    "contraction": float(np.median(st[:, 44] - st[:, 43])),
                    "epilogue": float(np.median(st[:, 45] - st[:, 44]))}
     blocks = {}
-    if args.ctl and np.all(st[:, 56] > 0):  # the assembly's blocks (slots 50..56, thread 0) from slot 5
+    if args.ctl and np.all(st[:, 51] > 0):  # the assembly's passes (slots 50-51, thread 0) from slot 5
         prev = st[:, 5]
-        for b in range(7):
-            blocks[f"block{b}"] = float(np.median(st[:, 50 + b] - prev))
+        for b, name in enumerate(("append", "shift")):
+            blocks[name] = float(np.median(st[:, 50 + b] - prev))
             prev = st[:, 50 + b]
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
