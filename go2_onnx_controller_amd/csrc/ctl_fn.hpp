@@ -133,8 +133,14 @@ struct CtlQ {
   Pro pro;
 };
 
+// The controller parameters are read through the constant address space: scalar
+// loads (lgkmcnt). Read through the generic pointer after the kernel's first store
+// they were vector loads, and the vmcnt(0) in front of their use also waited for the
+// weight fragments the pipeline keeps in flight across the input staging.
+typedef const __attribute__((address_space(4))) DevCtlParams kparams_t;
+
 __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
-  const DevCtlParams &Q = *C.prm;
+  kparams_t &Q = *(kparams_t *)C.prm;
   return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2], P.in_dim, P.in_pad,
               pro_of(P)};
 }
@@ -152,7 +158,7 @@ __device__ __forceinline__ int ctl_width(int b) { return b < 3 ? 3 : (b < 6 ? 12
 // may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k]. NaN among the
 // appended values of blocks 0-5 — where the reference's populate_buffer check
 // exit(1)s (controller.hpp:57-64) — sets nanf[r].
-template <bool TILE>
+template <bool TILE, bool ARITH>
 __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool joy, int nrows, float *__restrict__ dst,
                                            int ds, float *__restrict__ raw, int tid, int nt) {
   // the LDS image, the destination and the caller's rows never overlap: without
@@ -195,7 +201,7 @@ __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool jo
     }
     if (b < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
     if (raw) raw[r * in_dim + k] = v;
-    dst[r * ds + k] = TILE ? prologue(q.pro, v, k) : v;
+    dst[r * ds + k] = !TILE ? v : (ARITH ? prologue(q.pro, v, k) : (q.pro.clip ? clip_nan(v, q.pro.lo, q.pro.hi) : v));
   }
 }
 
@@ -204,7 +210,7 @@ __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool jo
 // block, shift and prologue constants worked out once, then UNR rows' loads in
 // flight at a time. TILE: dst is the batched kernel's LDS tile — its padding
 // columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too.
-template <bool TILE, int UNR>
+template <bool TILE, bool ARITH, int UNR>
 __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrows, float *__restrict__ dst, int ds,
                                           float *__restrict__ raw, int tid, int nt) {
   const float *__restrict__ obs_l = L.obs;
@@ -217,12 +223,13 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrow
     const int b = (k >= 3 * H) + (k >= 6 * H) + (k >= 9 * H) + (k >= 21 * H) + (k >= 33 * H) + (k >= 45 * H);
     const int cum = ctl_cum(b), d = ctl_width(b);
     if (k - H * cum >= (H - 1) * d) continue;  // an appended column (ctl_append)
-    const ProK pk = pro_k(q.pro, k);
+    const ProK pk = ARITH ? pro_k(q.pro, k) : ProK{0.f, 1.f, 1.f};
 #pragma unroll UNR
     for (int r = 0; r < nrows; ++r) {
       const float v = obs_l[r * in_dim + k + d];
       if (raw) raw[r * in_dim + k] = v;
-      dst[r * ds + k] = TILE ? prologue(q.pro, pk, v) : v;
+      dst[r * ds + k] =
+          !TILE ? v : (ARITH ? prologue(q.pro, pk, v) : (q.pro.clip ? clip_nan(v, q.pro.lo, q.pro.hi) : v));
     }
   }
   if constexpr (TILE)
@@ -239,14 +246,23 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrow
 // history blocks one after another, each element deriving its row, block and
 // source by division: ~10K cycles per 16-robot tile at 4 waves.)
 // UNR: rows in flight per thread in the shift pass (fewer where registers are
-// scarce: the resident kernels).
+// scarce: the resident kernels). A prologue with per-column arithmetic (ARITH) reads
+// its constants from global memory; without one the passes touch only LDS and the
+// caller's rows, so the compiler puts no vmcnt wait among them (such a wait also
+// waited for the pipeline's weight fragments in flight and for the rows' stores).
 template <bool TILE, int UNR = 8>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
   // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
-  ctl_append<TILE>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  GO2PI_STAMP(P, tid == 0, 50);
-  ctl_shift<TILE, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
+  if (TILE && (q.pro.sub || q.pro.div || q.pro.mul)) {
+    ctl_append<TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+    GO2PI_STAMP(P, tid == 0, 50);
+    ctl_shift<TILE, true, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
+  } else {
+    ctl_append<TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+    GO2PI_STAMP(P, tid == 0, 50);
+    ctl_shift<TILE, false, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
+  }
   GO2PI_STAMP(P, tid == 0, 51);
 }
 
@@ -264,7 +280,7 @@ struct CtlView {
 };
 
 __device__ __forceinline__ CtlView ctl_view(const DevCtl C, const CtlLds L, int row0) {
-  const DevCtlParams &Q = *C.prm;
+  kparams_t &Q = *(kparams_t *)C.prm;
   return CtlView{C.action, C.q_des, C.kp, C.kd, L.q0, C.joy ? L.jy : nullptr, Q.action_scale, Q.kp_run,
                  Q.kp_stop, Q.kd_run, Q.action_limit, row0, 1};
 }

@@ -1227,7 +1227,8 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   GO2PI_STAMP(P, lane == 0 && step == 0 && wave == 0, 6);
   float *Y = Y0;  // where the previous layer's activations go
   const ActP ap{hot.hid_act, hot.hid_alpha, hot.hid_beta};
-#pragma unroll(NHC > 0 ? NHC : 1)
+  constexpr int kHidUnroll = NHC > 0 ? NHC : 1;
+#pragma unroll kHidUnroll
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
     const WStream ws(w4_layer_w<TPW>(hot, l)), wn(w4_layer_w<TPW>(hot, more ? l + 1 : l));
