@@ -154,10 +154,15 @@ __device__ __forceinline__ int ctl_width(int b) { return b < 3 ? 3 : (b < 6 ? 12
 
 // The appended values of rows r < nrows: element (i, r) of the 49 x rows grid
 // (row index fastest, so a wave's lanes share one or two blocks' code). Per
-// element: the raw value goes to raw[r * in_dim + k] (the tile's global obs rows;
-// may be null) and TILE ? prologue(raw) : raw to dst[r * ds + k]. NaN among the
-// appended values of blocks 0-5 — where the reference's populate_buffer check
-// exit(1)s (controller.hpp:57-64) — sets nanf[r].
+// element: the raw value goes to raw[r * in_dim + k] (TILE: the tile's global obs
+// rows; the other callers pass none) and TILE ? prologue(raw) : raw to
+// dst[r * ds + k]. NaN among the appended values of blocks 0-5 — where the
+// reference's populate_buffer check exit(1)s (controller.hpp:57-64) — sets nanf[r].
+// Four elements per thread at a time: every element's one LDS read (the copied
+// value, or a stand-in where gravity and the joystick need more) is issued before
+// any is used, and the per-block work is selects plus two short branches. (With a
+// branch per block and each read waited for where it was issued, a thread's three
+// or four elements took ~4.5K cycles at 4 waves: one wave per SIMD hides nothing.)
 template <bool TILE, bool ARITH>
 __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool joy, int nrows, float *__restrict__ dst,
                                            int ds, float *__restrict__ raw, int tid, int nt) {
@@ -167,49 +172,70 @@ __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool jo
   const float *__restrict__ st_l = L.st;
   const float *__restrict__ jy_l = L.jy;
   const float *__restrict__ act_l = L.act;
+  const double *__restrict__ q0_l = L.q0;
   const int H = q.hist, in_dim = q.in_dim;
   const int lg = nrows <= 1 ? 0 : 32 - __builtin_clz(nrows - 1);
-  for (int e = tid; e < (GO2PI_CTL_STEP_DIM << lg); e += nt) {
-    const int r = e & ((1 << lg) - 1), i = e >> lg;
-    if (r >= nrows) continue;
-    const int b = (i >= 3) + (i >= 6) + (i >= 9) + (i >= 21) + (i >= 33) + (i >= 45);
-    const int cum = ctl_cum(b), d = ctl_width(b), c = i - cum;
-    const int k = H * cum + (H - 1) * d + c;
-    const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
-    float v;
-    if (b == 0) {
-      v = ctl_gravity(st, q.g0, q.g1, q.g2, c);
-    } else if (b == 1) {
-      v = st[4 + c];  // imu gyroscope (controller.hpp:105-109)
-    } else if (b == 2) {  // vel_cmd from the joystick (controller.cpp:173-179), kept without axes
-      const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
-      if (!joy || jy[0] == 0.f) v = obs_l[r * in_dim + k];  // the previous tick's vel_cmd_
-      else if (c == 0) v = jy[2];                           // axes[1]
-      else if (c == 2) v = jy[3] * jy[2];                   // axes[3] * axes[1]
-      else {                                                // pow(axes[0], 2) * sign * 0.8 in double
-        const double a0 = jy[1];
-        v = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
-      }
-    } else if (b == 3) {
-      v = (float)((double)st[7 + c] - L.q0[c]);  // q_[i] -= q0_[i] (double q0_)
-    } else if (b == 4) {
-      v = st[19 + c];
-    } else if (b == 5) {
-      v = act_l[r * GO2PI_CTL_DOF + c];  // action_ before act()
-    } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
-      v = st[31 + (c ^ 1)] >= q.thr ? 1.f : 0.f;
+  const int total = GO2PI_CTL_STEP_DIM << lg;
+  constexpr int U = 4;
+  for (int e0 = tid; e0 < total; e0 += U * nt) {
+    float v[U];
+    double q0c[U];
+    int rr[U], bb[U], cc[U], kk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nt;
+      const int r = e & ((1 << lg) - 1), i = e >> lg;
+      const bool ok = e < total && r < nrows;
+      const int b = ok ? (i >= 3) + (i >= 6) + (i >= 9) + (i >= 21) + (i >= 33) + (i >= 45) : 7;
+      const int cum = ctl_cum(b), d = ctl_width(b), c = i - cum;
+      const int k = H * cum + (H - 1) * d + c;
+      // the block's source value: gyro st[4 + c], q st[7 + c], dq st[19 + c], the
+      // previous action, foot force st[31 + (c ^ 1)] (FL/FR, RL/RR swap,
+      // controller.hpp:99-103), the previous vel_cmd_ (kept without joystick axes)
+      const float *src = b == 5 ? act_l + r * GO2PI_CTL_DOF + c
+                         : b == 2 ? obs_l + r * in_dim + k
+                                  : st_l + r * GO2PI_CTL_STATE_DIM +
+                                        (b == 1 ? 4 + c : b == 3 ? 7 + c : b == 4 ? 19 + c : b == 6 ? 31 + (c ^ 1) : 0);
+      v[u] = ok ? *src : 0.f;
+      q0c[u] = q0_l[b == 3 ? c : 0];
+      rr[u] = r;
+      bb[u] = b;
+      cc[u] = c;
+      kk[u] = k;
     }
-    if (b < 6 && __builtin_isnan(v)) atomicOr(L.nanf + r, 1u);
-    if (raw) raw[r * in_dim + k] = v;
-    dst[r * ds + k] = !TILE ? v : (ARITH ? prologue(q.pro, v, k) : (q.pro.clip ? clip_nan(v, q.pro.lo, q.pro.hi) : v));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rr[u], b = bb[u], c = cc[u], k = kk[u];
+      if (b == 7) continue;
+      float x = v[u];
+      if (b == 0) {
+        x = ctl_gravity(st_l + r * GO2PI_CTL_STATE_DIM, q.g0, q.g1, q.g2, c);
+      } else if (b == 2 && joy) {  // vel_cmd from the joystick (controller.cpp:173-179)
+        const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
+        if (jy[0] != 0.f) {
+          if (c == 0) x = jy[2];               // axes[1]
+          else if (c == 2) x = jy[3] * jy[2];  // axes[3] * axes[1]
+          else {                               // pow(axes[0], 2) * sign * 0.8 in double
+            const double a0 = jy[1];
+            x = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
+          }
+        }
+      }
+      if (b == 3) x = (float)((double)x - q0c[u]);  // q_[i] -= q0_[i] (double q0_)
+      if (b == 6) x = x >= q.thr ? 1.f : 0.f;       // foot_force >= 22
+      if (b < 6 && __builtin_isnan(x)) atomicOr(L.nanf + r, 1u);
+      if constexpr (TILE) raw[r * in_dim + k] = x;
+      dst[r * ds + k] = !TILE ? x : (ARITH ? prologue(q.pro, x, k) : (q.pro.clip ? clip_nan(x, q.pro.lo, q.pro.hi) : x));
+    }
   }
 }
 
 // The shifted values (std::shift_left by d, controller.hpp:45-52): column k of
 // every row r < nrows takes the image's column k + d. One column per thread, its
-// block, shift and prologue constants worked out once, then UNR rows' loads in
-// flight at a time. TILE: dst is the batched kernel's LDS tile — its padding
-// columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too.
+// block, shift and prologue constants worked out once, then UNR rows' LDS reads
+// issued before any of their stores. TILE: dst is the batched kernel's LDS tile —
+// its padding columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too — and
+// the raw values go to the tile's global obs rows.
 template <bool TILE, bool ARITH, int UNR>
 __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrows, float *__restrict__ dst, int ds,
                                           float *__restrict__ raw, int tid, int nt) {
@@ -224,13 +250,20 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrow
     const int cum = ctl_cum(b), d = ctl_width(b);
     if (k - H * cum >= (H - 1) * d) continue;  // an appended column (ctl_append)
     const ProK pk = ARITH ? pro_k(q.pro, k) : ProK{0.f, 1.f, 1.f};
-#pragma unroll UNR
-    for (int r = 0; r < nrows; ++r) {
-      const float v = obs_l[r * in_dim + k + d];
-      if (raw) raw[r * in_dim + k] = v;
-      dst[r * ds + k] =
-          !TILE ? v : (ARITH ? prologue(q.pro, pk, v) : (q.pro.clip ? clip_nan(v, q.pro.lo, q.pro.hi) : v));
+    auto put = [&](int r, float x) {
+      if constexpr (TILE) raw[r * in_dim + k] = x;
+      dst[r * ds + k] = !TILE ? x : (ARITH ? prologue(q.pro, pk, x) : (q.pro.clip ? clip_nan(x, q.pro.lo, q.pro.hi) : x));
+    };
+    const float *col = obs_l + k + d;
+    int r = 0;
+    for (; r + UNR <= nrows; r += UNR) {
+      float x[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) x[u] = col[(r + u) * in_dim];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) put(r + u, x[u]);
     }
+    for (; r < nrows; ++r) put(r, col[r * in_dim]);
   }
   if constexpr (TILE)
     for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * q.in_pad; e += nt) {
@@ -250,7 +283,7 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrow
 // its constants from global memory; without one the passes touch only LDS and the
 // caller's rows, so the compiler puts no vmcnt wait among them (such a wait also
 // waited for the pipeline's weight fragments in flight and for the rows' stores).
-template <bool TILE, int UNR = 8>
+template <bool TILE, int UNR = 16>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
   // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
@@ -264,6 +297,12 @@ __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const Ctl
     ctl_shift<TILE, false, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
   }
   GO2PI_STAMP(P, tid == 0, 51);
+#ifdef GO2PI_DIAG_ASM2  // both passes again, warm (instruction fetch vs. work): slots 52-53
+  ctl_append<TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 52);
+  ctl_shift<TILE, false, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
+  GO2PI_STAMP(P, tid == 0, 53);
+#endif
 }
 
 // What the final layer's store needs (controller tick), by value: the call's
@@ -287,6 +326,7 @@ __device__ __forceinline__ CtlView ctl_view(const DevCtl C, const CtlLds L, int 
 
 // Action post-processing of robot `row`, joint n (controller.cpp:217-223, 240-248).
 __device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float v) {
+#pragma clang fp contract(off)  // q_des: a product then a sum, two roundings, as the reference's x86 build
   float a = v < -V.lim ? -V.lim : (V.lim < v ? V.lim : v);  // std::clamp (NaN passes through)
   const bool stop = V.jy && V.jy[(row - V.row0) * GO2PI_CTL_JOY_DIM + 4] != 0.f;
   a *= stop ? 0.f : 1.f;  // a *= joy_->buttons[0] == 0

@@ -208,7 +208,7 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
       const float *src = obs;
       if constexpr (CTL) {
         __syncthreads();  // the LDS image of the inputs (and the weights above) landed
-        ctl_assemble_flat<false>(P, CL, cq, ctl.joy != nullptr, B, okeep, P.in_dim, nullptr, tid, LAT_WAVES * 64);
+        ctl_assemble_flat<false, 4>(P, CL, cq, ctl.joy != nullptr, B, okeep, P.in_dim, nullptr, tid, LAT_WAVES * 64);
         __syncthreads();
         src = okeep;
       }

@@ -453,7 +453,7 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
         if (tid < GO2PI_CTL_DOF) CL.q0[tid] = C.prm->q0[tid];
         if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
         __syncthreads();
-        ctl_assemble_flat<false>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, RES_WAVES * 64);
+        ctl_assemble_flat<false, 4>(P, CL, ctl_q(P, C), joy, B, obsv, in_dim, nullptr, tid, RES_WAVES * 64);
         __syncthreads();
         if (wave == 0) {  // mirror the assembled observation for the other workgroups
           for (int i = lane; i < B * in_dim; i += 64)

@@ -90,7 +90,8 @@ def main():
     blocks = {}
     if args.ctl and np.all(st[:, 51] > 0):  # the assembly's passes (slots 50-51, thread 0) from slot 5
         prev = st[:, 5]
-        for b, name in enumerate(("append", "shift")):
+        names = ("append", "shift") + (("append_again", "shift_again") if np.all(st[:, 53] > 0) else ())
+        for b, name in enumerate(names):  # (the _again passes: GO2PI_DIAG_ASM2 builds)
             blocks[name] = float(np.median(st[:, 50 + b] - prev))
             prev = st[:, 50 + b]
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
