@@ -152,124 +152,133 @@ __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
 __device__ __forceinline__ int ctl_cum(int b) { return b < 3 ? 3 * b : (b < 6 ? 9 + 12 * (b - 3) : 45); }
 __device__ __forceinline__ int ctl_width(int b) { return b < 3 ? 3 : (b < 6 ? 12 : 4); }
 
-// The appended values of rows r < nrows: element (i, r) of the 49 x rows grid
-// (row index fastest, so a wave's lanes share one or two blocks' code). Per
-// element: the raw value goes to raw[r * in_dim + k] (TILE: the tile's global obs
-// rows; the other callers pass none) and TILE ? prologue(raw) : raw to
-// dst[r * ds + k]. NaN among the appended values of blocks 0-5 — where the
-// reference's populate_buffer check exit(1)s (controller.hpp:57-64) — sets nanf[r].
-// Four elements per thread at a time: every element's one LDS read (the copied
-// value, or a stand-in where gravity and the joystick need more) is issued before
-// any is used, and the per-block work is selects plus two short branches. (With a
-// branch per block and each read waited for where it was issued, a thread's three
-// or four elements took ~4.5K cycles at 4 waves: one wave per SIMD hides nothing.)
+// Prologue of one observation value (TILE: the batched kernel's layer-0 tile);
+// ARITH: the prologue has per-column arithmetic (constants read from global memory).
 template <bool TILE, bool ARITH>
-__device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ q, bool joy, int nrows, float *__restrict__ dst,
-                                           int ds, float *__restrict__ raw, int tid, int nt) {
-  // the LDS image, the destination and the caller's rows never overlap: without
-  // __restrict__ every element's reads waited behind the previous element's stores
+__device__ __forceinline__ float ctl_pro(const CtlQ &q, float x, int k) {
+  if constexpr (!TILE) return x;
+  else if constexpr (ARITH) return prologue(q.pro, x, k);
+  else return q.pro.clip ? clip_nan(x, q.pro.lo, q.pro.hi) : x;
+}
+
+// The values block BK appends to rows r < nrows (element e = r * d + c), with
+// straight-line code per block and no per-element branch: one wave per SIMD has no
+// other wave to cover the exec-mask round trips of a divergent if-chain (a generic
+// per-element form took ~5K cycles for 16 rows at 4 waves). The thread -> element
+// map is rotated by 64 * BK so that the small blocks start on different waves.
+// The raw value goes to raw[r * in_dim + k] (TILE: the tile's global obs rows) and
+// its prologue value to dst[r * ds + k]. NaN among the appended values of blocks
+// 0-5 — where the reference's populate_buffer check exit(1)s
+// (controller.hpp:57-64) — sets nanf[r] (a relaxed workgroup-scope LDS or: no fence).
+template <int BK, bool TILE, bool ARITH>
+__device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, bool joy, int nrows,
+                                                 float *__restrict__ dst, int ds, float *__restrict__ raw, int tid,
+                                                 int nt) {
   const float *__restrict__ obs_l = L.obs;
   const float *__restrict__ st_l = L.st;
   const float *__restrict__ jy_l = L.jy;
   const float *__restrict__ act_l = L.act;
-  const double *__restrict__ q0_l = L.q0;
+  constexpr int d = BK < 3 ? 3 : (BK < 6 ? 12 : 4);
+  constexpr int cum = BK < 3 ? 3 * BK : (BK < 6 ? 9 + 12 * (BK - 3) : 45);
   const int H = q.hist, in_dim = q.in_dim;
-  const int lg = nrows <= 1 ? 0 : 32 - __builtin_clz(nrows - 1);
-  const int total = GO2PI_CTL_STEP_DIM << lg;
-  constexpr int U = 4;
-  for (int e0 = tid; e0 < total; e0 += U * nt) {
-    float v[U];
-    double q0c[U];
-    int rr[U], bb[U], cc[U], kk[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = e0 + u * nt;
-      const int r = e & ((1 << lg) - 1), i = e >> lg;
-      const bool ok = e < total && r < nrows;
-      const int b = ok ? (i >= 3) + (i >= 6) + (i >= 9) + (i >= 21) + (i >= 33) + (i >= 45) : 7;
-      const int cum = ctl_cum(b), d = ctl_width(b), c = i - cum;
-      const int k = H * cum + (H - 1) * d + c;
-      // the block's source value: gyro st[4 + c], q st[7 + c], dq st[19 + c], the
-      // previous action, foot force st[31 + (c ^ 1)] (FL/FR, RL/RR swap,
-      // controller.hpp:99-103), the previous vel_cmd_ (kept without joystick axes)
-      const float *src = b == 5 ? act_l + r * GO2PI_CTL_DOF + c
-                         : b == 2 ? obs_l + r * in_dim + k
-                                  : st_l + r * GO2PI_CTL_STATE_DIM +
-                                        (b == 1 ? 4 + c : b == 3 ? 7 + c : b == 4 ? 19 + c : b == 6 ? 31 + (c ^ 1) : 0);
-      v[u] = ok ? *src : 0.f;
-      q0c[u] = q0_l[b == 3 ? c : 0];
-      rr[u] = r;
-      bb[u] = b;
-      cc[u] = c;
-      kk[u] = k;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = rr[u], b = bb[u], c = cc[u], k = kk[u];
-      if (b == 7) continue;
-      float x = v[u];
-      if (b == 0) {
-        x = ctl_gravity(st_l + r * GO2PI_CTL_STATE_DIM, q.g0, q.g1, q.g2, c);
-      } else if (b == 2 && joy) {  // vel_cmd from the joystick (controller.cpp:173-179)
+  const int k0 = H * cum + (H - 1) * d;  // the block's first appended column
+  int t = tid - (64 * BK) % nt;
+  if (t < 0) t += nt;
+  for (int e = t; e < nrows * d; e += nt) {
+    const int r = e / d, c = e - r * d, k = k0 + c;
+    const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
+    float x;
+    if constexpr (BK == 0) {
+      x = ctl_gravity(st, q.g0, q.g1, q.g2, c);
+    } else if constexpr (BK == 1) {
+      x = st[4 + c];  // imu gyroscope (controller.hpp:105-109)
+    } else if constexpr (BK == 2) {
+      // vel_cmd from the joystick (controller.cpp:173-179); kept (the previous
+      // tick's vel_cmd_) without a joystick or without axes
+      x = obs_l[r * in_dim + k];
+      if (joy) {
         const float *jy = jy_l + r * GO2PI_CTL_JOY_DIM;
-        if (jy[0] != 0.f) {
-          if (c == 0) x = jy[2];               // axes[1]
-          else if (c == 2) x = jy[3] * jy[2];  // axes[3] * axes[1]
-          else {                               // pow(axes[0], 2) * sign * 0.8 in double
-            const double a0 = jy[1];
-            x = (float)(a0 * a0 * (jy[1] > 0.f ? 1.0 : -1.0) * 0.8);
-          }
-        }
+        const float j0 = jy[0], a0 = jy[1], a1 = jy[2], a3 = jy[3];
+        const double a0d = a0;
+        const float sq = (float)(a0d * a0d * (a0 > 0.f ? 1.0 : -1.0) * 0.8);  // pow(axes[0], 2) * sign * 0.8
+        const float cmd = c == 0 ? a1 : (c == 2 ? a3 * a1 : sq);               // axes[1], axes[3] * axes[1]
+        x = j0 != 0.f ? cmd : x;
       }
-      if (b == 3) x = (float)((double)x - q0c[u]);  // q_[i] -= q0_[i] (double q0_)
-      if (b == 6) x = x >= q.thr ? 1.f : 0.f;       // foot_force >= 22
-      if (b < 6 && __builtin_isnan(x)) atomicOr(L.nanf + r, 1u);
-      if constexpr (TILE) raw[r * in_dim + k] = x;
-      dst[r * ds + k] = !TILE ? x : (ARITH ? prologue(q.pro, x, k) : (q.pro.clip ? clip_nan(x, q.pro.lo, q.pro.hi) : x));
+    } else if constexpr (BK == 3) {
+      x = (float)((double)st[7 + c] - L.q0[c]);  // q_[i] -= q0_[i] (double q0_)
+    } else if constexpr (BK == 4) {
+      x = st[19 + c];
+    } else if constexpr (BK == 5) {
+      x = act_l[r * GO2PI_CTL_DOF + c];  // action_ before act()
+    } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
+      x = st[31 + (c ^ 1)] >= q.thr ? 1.f : 0.f;
     }
+    if constexpr (BK < 6)
+      __hip_atomic_fetch_or(L.nanf + r, __builtin_isnan(x) ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (TILE) raw[r * in_dim + k] = x;
+    dst[r * ds + k] = ctl_pro<TILE, ARITH>(q, x, k);
   }
 }
 
+template <bool TILE, bool ARITH>
+__device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ &q, bool joy, int nrows, float *__restrict__ dst,
+                                           int ds, float *__restrict__ raw, int tid, int nt) {
+  ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<2, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<4, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<5, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  ctl_append_block<6, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+}
+
 // The shifted values (std::shift_left by d, controller.hpp:45-52): column k of
-// every row r < nrows takes the image's column k + d. One column per thread, its
-// block, shift and prologue constants worked out once, then UNR rows' LDS reads
-// issued before any of their stores. TILE: dst is the batched kernel's LDS tile —
-// its padding columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too — and
-// the raw values go to the tile's global obs rows.
-template <bool TILE, bool ARITH, int UNR>
-__device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrows, float *__restrict__ dst, int ds,
+// every row r < nrows takes the image's column k + d. The (H - 1) * 49 shifted
+// columns of all rows are one flat range (row-major, so a wave's reads and the
+// caller's row stores are contiguous), U elements per thread in flight: every LDS
+// read issued before the first store. TILE: dst is the batched kernel's LDS tile
+// — its padding columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too.
+template <bool TILE, bool ARITH, int U>
+__device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nrows, float *__restrict__ dst, int ds,
                                           float *__restrict__ raw, int tid, int nt) {
   const float *__restrict__ obs_l = L.obs;
-  const int H = q.hist, in_dim = q.in_dim, kend = TILE ? q.in_pad : in_dim;
-  for (int k = tid; k < kend; k += nt) {
-    if (k >= in_dim) {
-      for (int r = 0; r < nrows; ++r) dst[r * ds + k] = 0.f;
-      continue;
-    }
-    const int b = (k >= 3 * H) + (k >= 6 * H) + (k >= 9 * H) + (k >= 21 * H) + (k >= 33 * H) + (k >= 45 * H);
-    const int cum = ctl_cum(b), d = ctl_width(b);
-    if (k - H * cum >= (H - 1) * d) continue;  // an appended column (ctl_append)
-    const ProK pk = ARITH ? pro_k(q.pro, k) : ProK{0.f, 1.f, 1.f};
-    auto put = [&](int r, float x) {
-      if constexpr (TILE) raw[r * in_dim + k] = x;
-      dst[r * ds + k] = !TILE ? x : (ARITH ? prologue(q.pro, pk, x) : (q.pro.clip ? clip_nan(x, q.pro.lo, q.pro.hi) : x));
-    };
-    const float *col = obs_l + k + d;
-    int r = 0;
-    for (; r + UNR <= nrows; r += UNR) {
-      float x[UNR];
+  const int H = q.hist, h1 = H - 1, in_dim = q.in_dim, nc = h1 * GO2PI_CTL_STEP_DIM, total = nrows * nc;
+  const float rnc = 1.f / (float)(nc > 0 ? nc : 1);
+  for (int e0 = tid; e0 < total; e0 += U * nt) {
+    float x[U];
+    int rr[U], kk[U];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) x[u] = col[(r + u) * in_dim];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) put(r + u, x[u]);
+    for (int u = 0; u < U; ++u) {
+      const int e = min(e0 + u * nt, total - 1);
+      // r = e / nc exactly: (e + 0.5) / nc is >= 0.5 / nc away from an integer and
+      // the float product's error is far below that here (nc <= 15 * 49, e < 16 nc)
+      const int r = (int)(((float)e + 0.5f) * rnc), j = e - r * nc;
+      // the j-th shifted column: block b holds (H - 1) * d of them from column H * cum
+      const int b = (j >= h1 * 3) + (j >= h1 * 6) + (j >= h1 * 9) + (j >= h1 * 21) + (j >= h1 * 33) + (j >= h1 * 45);
+      const int cum = ctl_cum(b), d = ctl_width(b);
+      const int k = H * cum + (j - h1 * cum);
+      rr[u] = r;
+      kk[u] = k;
+      x[u] = obs_l[r * in_dim + k + d];
     }
-    for (; r < nrows; ++r) put(r, col[r * in_dim]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e0 + u * nt >= total) break;
+      if constexpr (TILE) raw[rr[u] * in_dim + kk[u]] = x[u];
+      dst[rr[u] * ds + kk[u]] = ctl_pro<TILE, ARITH>(q, x[u], kk[u]);
+    }
   }
-  if constexpr (TILE)
+  if constexpr (TILE) {
+    const int pw = q.in_pad - in_dim;
+    for (int e = tid; e < nrows * pw; e += nt) {
+      const int r = e / pw;
+      dst[r * ds + in_dim + (e - r * pw)] = 0.f;
+    }
     for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * q.in_pad; e += nt) {
       const int r = nrows + e / q.in_pad;
       dst[r * ds + (e - (r - nrows) * q.in_pad)] = 0.f;
     }
+  }
 }
 
 // Assemble this tick's observation rows r < nrows from the LDS image (needs the
@@ -278,12 +287,12 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ q, int nrow
 // the two passes need no barrier between them. (The earlier form ran the seven
 // history blocks one after another, each element deriving its row, block and
 // source by division: ~10K cycles per 16-robot tile at 4 waves.)
-// UNR: rows in flight per thread in the shift pass (fewer where registers are
-// scarce: the resident kernels). A prologue with per-column arithmetic (ARITH) reads
+// UNR: elements in flight per thread in the shift pass (fewer where registers
+// are scarce: the resident kernels). A prologue with per-column arithmetic (ARITH) reads
 // its constants from global memory; without one the passes touch only LDS and the
 // caller's rows, so the compiler puts no vmcnt wait among them (such a wait also
 // waited for the pipeline's weight fragments in flight and for the rows' stores).
-template <bool TILE, int UNR = 16>
+template <bool TILE, int UNR = 4>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
   // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
