@@ -1347,6 +1347,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) hs[0] += scratch[(wave * 4 + w) * 64 + lane];
+    GO2PI_STAMP(P, lane == 0 && wave == 0 && step == 0, 54);  // tail marks: 54 partials summed, 55 stored
     // no action post-processing (the lean kernel; a general-body program without
     // tanh / clip / scale, e.g. a GRU policy): the head's activation (usually none)
     // and the plain store of the valid rows / columns, from the hot fields
@@ -1367,6 +1368,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       float4 none[1];
       dense_store<1>(P, P.L[nh], hs, hbv, wave, HT, lane, true, nullptr, 0, ac, cv, row0, B, none);
     }
+    GO2PI_STAMP(P, lane == 0 && wave == 0 && step == 0, 55);
   }
 }
 

@@ -94,6 +94,11 @@ def main():
         for b, name in enumerate(names):  # (the _again passes: GO2PI_DIAG_ASM2 builds)
             blocks[name] = float(np.median(st[:, 50 + b] - prev))
             prev = st[:, 50 + b]
+    if np.all(st[:, 55] > 0):  # the pipeline's head tail (wave 0): partials summed, stored, from the head barrier
+        hb = st[:, 6 + nl - 1]
+        blocks["tail_partials"] = float(np.median(st[:, 54] - hb))
+        blocks["tail_store"] = float(np.median(st[:, 55] - st[:, 54]))
+        blocks["tail_end"] = float(np.median(st[:, 2] - st[:, 55]))
     if args.ctl:  # slot 5: inputs staged in LDS, 4: obs assembled, 15: obs published
         marks = [st[:, 0], st[:, 5], st[:, 4], st[:, 15]] + [st[:, 6 + l] for l in range(nl)] + [st[:, 2]]
         names = ["ctl_load", "assemble", "publish"] + [f"layer{l}" for l in range(nl)] + ["tail"]
