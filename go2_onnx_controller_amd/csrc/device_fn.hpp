@@ -111,11 +111,22 @@ __device__ __forceinline__ void with_act(int act, F &&f) {
 
 // The action epilogue (go2pi_opts and a graph's trailing Clip / scalar Mul):
 // y <- scale * clip(tanh?(y), lo, hi); the clip passes a NaN through, as ONNX Clip.
-__device__ __forceinline__ float post_fn(const DevProgram &P, float v) {
-  if (P.post_tanh) v = tanhf(v);
-  v = clip_nan(v, P.clip_lo, P.clip_hi);
-  return v * P.scale;
+// Post: its program fields read once, by value — a loop that stores the actions
+// would otherwise reload them (and wait for the scalar load) per element.
+struct Post {
+  int tanh;
+  float lo, hi, scale;
+};
+
+__device__ __forceinline__ Post post_of(const DevProgram &P) { return Post{P.post_tanh, P.clip_lo, P.clip_hi, P.scale}; }
+
+__device__ __forceinline__ float post_fn(const Post &q, float v) {
+  if (q.tanh) v = tanhf(v);
+  v = clip_nan(v, q.lo, q.hi);
+  return v * q.scale;
 }
+
+__device__ __forceinline__ float post_fn(const DevProgram &P, float v) { return post_fn(post_of(P), v); }
 
 // The prologue's program fields, read once (by value): loops that store to memory
 // between elements would otherwise reload them, and a reload the compiler cannot

@@ -230,6 +230,9 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
                                             float *Y, int ys, float *out, const CtlView ctl, int row0, int B,
                                             float4 (&keep)[TPW]) {
   const int rob = lane & 15, n0 = (lane >> 4) << 2;
+  // fields read once (the final layer's stores would make every element reload them)
+  const int LN = L.N;
+  const Post po = post_of(P);
   with_act(L.act, [&](auto act_k) {
     constexpr int ACT = decltype(act_k)::value;
     const ActP ap{L.act, L.alpha, L.beta};
@@ -251,10 +254,10 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = t * 16 + n0 + r;
-          if (n >= L.N) continue;
-          const float y = post_fn(P, f4c(v, r));
+          if (n >= LN) continue;
+          const float y = post_fn(po, f4c(v, r));
           if (ctl.on) ctl_store(ctl, row, n, y);  // controller tick: action post-processing
-          else out[(size_t)row * L.N + n] = y;
+          else out[(size_t)row * LN + n] = y;
         }
       }
     }

@@ -259,14 +259,17 @@ __device__ __forceinline__ void latency_body(const DevProgram &P, const float *o
     if (wave == LAT_PW && lane < 16) {
       const int n = g * 16 + lane;
       const bool last = l == P.nl - 1;
+      const int la = L.act, LN = L.N;  // (read once: the stores below would make each row reload them)
+      const float lal = L.alpha, lbe = L.beta;
+      const Post po = post_of(P);
       for (int b = 0; b < B; ++b) {
         float s = 0.f;
         for (int w2 = 0; w2 < LAT_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
-        const float v = act_fn(L.act, L.alpha, L.beta, s + bv);
+        const float v = act_fn(la, lal, lbe, s + bv);
         if (last) {
-          if (n < L.N) {
-            if constexpr (CTL) ctl_store(cv, b, n, post_fn(P, v));
-            else act[(size_t)b * L.N + n] = post_fn(P, v);
+          if (n < LN) {
+            if constexpr (CTL) ctl_store(cv, b, n, post_fn(po, v));
+            else act[(size_t)b * LN + n] = post_fn(po, v);
           }
           if (!CTL && done && b == B - 1 && g == 0) {
             // completion word for the host's spin (instead of a stream sync): every

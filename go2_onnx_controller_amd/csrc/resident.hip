@@ -667,22 +667,25 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
       if (wave == RES_PW && lane < 16) {
         const int n = g * 16 + lane;
         const bool lastl = l == P.nl - 1;
+        const int la = L.act, LN = L.N, LNP = L.N_pad;  // (read once: the stores below would make each row reload them)
+        const float lal = L.alpha, lbe = L.beta;
+        const Post po = post_of(P);
         for (int b = 0; b < B; ++b) {
           float s = 0.f;
           for (int w2 = 0; w2 < RES_WAVES; ++w2) s += part[(w2 * GO2PI_SMALL_MAXB + b) * 16 + lane];
-          const float v = act_fn(L.act, L.alpha, L.beta, s + bcur);
+          const float v = act_fn(la, lal, lbe, s + bcur);
           if (lastl) {
             if constexpr (CTL) {
-              if (n < L.N) ctl_store(cv, b, n, post_fn(P, v));
-            } else if (n < L.N) {
+              if (n < LN) ctl_store(cv, b, n, post_fn(po, v));
+            } else if (n < LN) {
               // the action as {epoch, value} granules in host memory: the host's spin reads
               // the data itself (no release drain, no done word behind it)
-              __hip_atomic_store(actg + (size_t)b * L.N + n, ((u64)e << 32) | __float_as_uint(post_fn(P, v)),
+              __hip_atomic_store(actg + (size_t)b * LN + n, ((u64)e << 32) | __float_as_uint(post_fn(po, v)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
           } else {
             const u64 gv = ((u64)(e + 1u + (unsigned)l) << 32) | __float_as_uint(v);
-            __hip_atomic_store(gran + (size_t)l * gstride + b * L.N_pad + n, gv, __ATOMIC_RELAXED,
+            __hip_atomic_store(gran + (size_t)l * gstride + b * LNP + n, gv, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
           }
         }

@@ -173,6 +173,7 @@ MODELS = {
     # controller-tick policies (49 * kHistory observations, 12 actions) besides the shipped 98 -> 12
     "ctl_h1": lambda: mlp_model_bytes((49, 64, 64, 12), seed=7),
     "ctl_h3": lambda: mlp_model_bytes((147, 128, 128, 12), seed=8),
+    "ctl_h16": lambda: mlp_model_bytes((784, 128, 128, 12), seed=17),  # the longest history (16 x 49)
     "gru_ctl": lambda: gru_model_bytes(I=98, H=64, head=(128, 12), seed=9),
     # shapes of the 4-wave pipeline (kernels.hip w4_step): tiles per wave x head tiles
     "pipe_256_h2": lambda: mlp_model_bytes((40, 256, 256, 20), seed=10),                      # 4 x 2, hand-off

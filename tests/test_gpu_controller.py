@@ -69,7 +69,7 @@ def test_controller_long_closed_loop_no_joystick():
         _run_ticks(e, _mlp_policy(SHIPPED), 16, 50, seed=11, joy_mode="none")
 
 
-@pytest.mark.parametrize("name,hist", [("ctl_h1", 1), ("ctl_h3", 3)])
+@pytest.mark.parametrize("name,hist", [("ctl_h1", 1), ("ctl_h3", 3), ("ctl_h16", 16)])
 @pytest.mark.parametrize("B", [5, 300])
 def test_controller_history_lengths(synth_path, name, hist, B):
     from go2_onnx_controller_amd import Engine
