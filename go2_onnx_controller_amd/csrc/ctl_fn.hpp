@@ -89,22 +89,26 @@ struct CtlLds {
   unsigned *nanf;
 };
 
-__host__ __device__ inline int ctl_lds_floats(int R, int in_dim) {
+// obs: the previous observation rows get a region of their own (false: the caller
+// places them, e.g. the batched kernel in its layer-0 output buffer, unused until the
+// assembly is done — at a 16-step history the rows are 50 KB per tile)
+__host__ __device__ inline int ctl_lds_floats(int R, int in_dim, bool obs = true) {
   auto c64 = [](int x) { return (x + 63) & ~63; };
   // q0: 12 doubles, copied by one direct-to-LDS instruction (64 lanes x 4 B: 64 floats of room)
-  return 64 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) + c64(R * in_dim) +
-         GO2PI_TILE_ROWS;
+  return 64 + c64(R * GO2PI_CTL_STATE_DIM) + c64(R * GO2PI_CTL_JOY_DIM) + c64(R * GO2PI_CTL_DOF) +
+         (obs ? c64(R * in_dim) : 0) + GO2PI_TILE_ROWS;
 }
 
-__device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim) {
+__device__ __forceinline__ CtlLds ctl_lds(float *base, int R, int in_dim, float *obs = nullptr) {
   auto c64 = [](int x) { return (x + 63) & ~63; };
   CtlLds L;
   L.q0 = reinterpret_cast<double *>(base);
   L.st = base + 64;
   L.jy = L.st + c64(R * GO2PI_CTL_STATE_DIM);
   L.act = L.jy + c64(R * GO2PI_CTL_JOY_DIM);
-  L.obs = L.act + c64(R * GO2PI_CTL_DOF);
-  L.nanf = reinterpret_cast<unsigned *>(L.obs + c64(R * in_dim));
+  float *end = L.act + c64(R * GO2PI_CTL_DOF);
+  L.obs = obs ? obs : end;
+  L.nanf = reinterpret_cast<unsigned *>(obs ? end : end + c64(R * in_dim));
   return L;
 }
 

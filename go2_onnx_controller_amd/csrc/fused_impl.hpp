@@ -1484,7 +1484,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   int ep = 0;  // hand-offs published so far (identical in every wave)
   // (the pipeline's bias copy sits between the flags and the controller-tick region)
   float *lbias = after_scratch + GO2PI_FLAG_FLOATS;
-  const CtlLds CL = ctl_lds(lbias + P.w4_bias, GO2PI_TILE_ROWS, P.in_dim);
+  // (the previous observation rows in bufB: layer 0's output buffer, written only after
+  // the assembly and the barrier behind it)
+  const CtlLds CL = ctl_lds(lbias + P.w4_bias, GO2PI_TILE_ROWS, P.in_dim, bufB);
   CtlView cv{};
   CtlQ cq{};
   // the pipeline without a recurrent cell assembles the tick's observation inside
@@ -1559,6 +1561,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       const int r = e / tail4;
       reinterpret_cast<float4 *>(bufA + r * S + P.in_pad)[e - r * tail4] = z;
     }
+    if constexpr (CTL) __syncthreads();  // every wave done reading the previous observation rows in bufB
     float4 *l4 = reinterpret_cast<float4 *>(bufB);
     const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
     for (int e = tid; e < n4; e += NT) l4[e] = z;
@@ -1727,7 +1730,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
 // rather than passed by value: a by-value kernarg is a fresh copy per launch, and
 // every cache line of it a workgroup first touches is a memory round trip.
 inline size_t fused_ctl_lds_bytes(const DevProgram &p, int waves) {
-  return fused_lds_bytes(p, waves) + sizeof(float) * ctl_lds_floats(GO2PI_TILE_ROWS, p.in_dim);
+  return fused_lds_bytes(p, waves) + sizeof(float) * ctl_lds_floats(GO2PI_TILE_ROWS, p.in_dim, false);
 }
 
 // The 4-wave pipeline's host side, one translation unit per tiles per wave
