@@ -5,6 +5,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
+mkdir -p gpurun_out/lat
 bash tools/gpu_tests.sh || exit 1
 bash tools/r04_latency.sh > gpurun_out/lat/r04_latency.log 2>&1 || { tail -20 gpurun_out/lat/r04_latency.log; exit 1; }
 echo latency done
