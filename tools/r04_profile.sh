@@ -10,6 +10,9 @@ TAG=mlp512 STEPS=300 ARGS="--no-cpu --no-latency --no-ctl --no-gru" bash tools/p
 TAG=gru256 STEPS=100 ARGS="--no-cpu --no-latency --no-ctl --no-gru --workload go2_gru_256_b4096" bash tools/profile.sh || exit 1
 TAG=gru256seq STEPS=40 ARGS="--no-cpu --no-latency --no-ctl --no-gru --workload go2_gru_256_b4096_seq100" bash tools/profile.sh || exit 1
 TAG=ctl STEPS=50 ARGS="--no-cpu --no-gru" bash tools/profile.sh || exit 1
+# keep what tools/summarize_prof.py reads (the per-dispatch traces would push gpurun_out
+# past what the box copies back)
+find gpurun_out -path '*prof_*' -type f ! -name 'run_kernel_stats.csv' ! -name 'run_counter_collection.csv' ! -name '*.log' -delete
 echo profiles done
 if [ -f go2_onnx_controller_amd/lib/diag/libgo2pi_clock.so ]; then
   export GO2PI_LIB=$PWD/go2_onnx_controller_amd/lib/diag/libgo2pi_clock.so GO2PI_DIAG_STAMPS=1
