@@ -350,4 +350,37 @@ __device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float
   if (V.kd) V.kd[o] = V.kd_run;
 }
 
+// The same for joints n .. n + 3 of one robot (n % 4 == 0, all four < 12): the
+// joystick row read once, and every output as 16-byte stores (the batched kernel's
+// head lane holds four consecutive joints). Per element the operations of ctl_store.
+__device__ __forceinline__ void ctl_store4(const CtlView V, int row, int n, const float (&v)[4]) {
+#pragma clang fp contract(off)
+  const bool stop = V.jy && V.jy[(row - V.row0) * GO2PI_CTL_JOY_DIM + 4] != 0.f;
+  float a[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = v[i] < -V.lim ? -V.lim : (V.lim < v[i] ? V.lim : v[i]);
+    a[i] *= stop ? 0.f : 1.f;
+  }
+  const size_t o = (size_t)row * GO2PI_CTL_DOF + n;
+  *reinterpret_cast<float4 *>(V.action + o) = make_float4(a[0], a[1], a[2], a[3]);
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  if (V.q_des) {
+    f64x2 q[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i >> 1][i & 1] = V.q0[n + i] + (double)a[i] * V.scale;
+    reinterpret_cast<f64x2 *>(V.q_des + o)[0] = q[0];
+    reinterpret_cast<f64x2 *>(V.q_des + o)[1] = q[1];
+  }
+  if (V.kp) {
+    const double k = stop ? V.kp_stop : V.kp_run;
+    reinterpret_cast<f64x2 *>(V.kp + o)[0] = f64x2{k, k};
+    reinterpret_cast<f64x2 *>(V.kp + o)[1] = f64x2{k, k};
+  }
+  if (V.kd) {
+    reinterpret_cast<f64x2 *>(V.kd + o)[0] = f64x2{V.kd_run, V.kd_run};
+    reinterpret_cast<f64x2 *>(V.kd + o)[1] = f64x2{V.kd_run, V.kd_run};
+  }
+}
+
 }  // namespace go2pi

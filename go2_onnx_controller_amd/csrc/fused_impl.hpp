@@ -251,6 +251,14 @@ __device__ __forceinline__ void dense_store(const DevProgram &P, const DevLayer 
       } else {
         const int row = row0 + rob;
         if (row >= B) continue;
+        if (ctl.on && LN == GO2PI_CTL_DOF) {  // controller tick: this lane's four joints at once
+          const int n = t * 16 + n0;
+          if (n < LN) {
+            const float y[4] = {post_fn(po, v.x), post_fn(po, v.y), post_fn(po, v.z), post_fn(po, v.w)};
+            ctl_store4(ctl, row, n, y);
+          }
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = t * 16 + n0 + r;
