@@ -1,6 +1,7 @@
 // "Controller-shaped" use of the drop-in header, exactly as the reference's
 // callers use it (onnx_controller/src/controller.cpp:25,49,215 with the
-// std::array members of controller.hpp:148-149; onnx_inference/src/cpp/main.cpp:32-45).
+// std::array members of controller.hpp:148-149; onnx_inference/src/cpp/main.cpp:26-45,
+// including the Ort::Env that main.cpp:26 creates before the actor).
 // Usage: controller_shape <model.onnx> [zeros|twos|ticks N [actions.bin]]
 //   ticks: N act() calls on an observation the caller changes in place before each
 //   (observation[t % 98] += 0.001f, as populate_buffer rewrites it every tick); with
@@ -10,7 +11,6 @@
 //   around one act()), over <warmup> untimed then <iters> timed calls on spans of
 //   the given sizes; prints p50 / p99 in microseconds.
 #include <algorithm>
-#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -26,6 +26,7 @@ constexpr size_t kHistory = 2;
 
 int main(int argc, char **argv) {
   if (argc < 2) return 2;
+  Ort::Env env(ORT_LOGGING_LEVEL_WARNING, "test");  // main.cpp:26
   std::array<float, kDimObs * kHistory> observation{};
   std::array<float, kDimDOF> action{};
   std::string mode = argc > 2 ? argv[2] : "zeros";
