@@ -289,14 +289,40 @@ struct go2pi_engine {
   // false: not served because the kernel kept being told to leave (a batched launch
   // on the device evicts live resident kernels, evict_residents): the caller serves
   // the request by a launch instead; the kernel is relaunched by a later call.
+  // go2pi_run's fast path makes no HIP call while a live kernel serves it (lazy_dev):
+  // need_device() switches the calling thread to the engine's device the first time a
+  // stop or relaunch needs the runtime, and dev_done() switches it back.
+  bool lazy_dev = false, dev_switched = false;
+  int dev_saved = -1;
+  void need_device() {
+    if (!lazy_dev || dev_switched) return;
+    if (hipGetDevice(&dev_saved) != hipSuccess) dev_saved = -1;
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    dev_switched = true;
+  }
+  void dev_done() {
+    if (dev_switched && dev_saved >= 0 && dev_saved != device) (void)hipSetDevice(dev_saved);
+    lazy_dev = dev_switched = false;
+  }
+  // the live kernel serves the next request as it is (no stop or relaunch due first)
+  bool resident_ready(const go2pi::DevCtl *ctl) const {
+    const auto idle = std::chrono::microseconds(1000LL * opts.resident_ms);
+    return resident_live && resident_ctl == (ctl != nullptr) && std::chrono::steady_clock::now() - res_last <= idle / 2 &&
+           __atomic_load_n(h_done, __ATOMIC_ACQUIRE) != GO2PI_RES_LEAVE &&
+           epoch <= 0xFFFFFFF0u - 2 * ((unsigned)prog.nl + 2);
+  }
   bool resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
-    if (resident_live && resident_ctl != (ctl != nullptr)) resident_stop();  // the other form is live
+    if (resident_live && resident_ctl != (ctl != nullptr)) {  // the other form is live
+      need_device();
+      resident_stop();
+    }
     const int n = (int)batch * (model.in_dim + (ctl ? GO2PI_CTL_RAW : 0));
     const auto idle = std::chrono::microseconds(1000LL * opts.resident_ms);  // (us: idle / 2 stays > 0 at 1 ms)
     for (int attempt = 0;; ++attempt) {
       // layer tags e + 1 + l: an epoch spans nl + 2 tags
       const unsigned span = (unsigned)prog.nl + 2;
       if (epoch > 0xFFFFFFF0u - 2 * span) {  // tag space exhausted: restart with zeroed granules
+        need_device();
         resident_stop();
         epoch = 1;
       }
@@ -305,9 +331,14 @@ struct go2pi_engine {
       last_epoch = e0;
       const auto now = std::chrono::steady_clock::now();
       // the kernel leaves after resident_ms idle: past half of it, relaunch rather than race its exit
-      if (resident_live && (now - res_last > idle / 2 || __atomic_load_n(h_done, __ATOMIC_ACQUIRE) == GO2PI_RES_LEAVE))
+      if (resident_live && (now - res_last > idle / 2 || __atomic_load_n(h_done, __ATOMIC_ACQUIRE) == GO2PI_RES_LEAVE)) {
+        need_device();
         resident_stop();
-      if (!resident_live) resident_start(ctl);
+      }
+      if (!resident_live) {
+        need_device();
+        resident_start(ctl);
+      }
       for (int i = 0; i < n; ++i) {
         unsigned bits;
         std::memcpy(&bits, rows + i, 4);
@@ -361,6 +392,7 @@ struct go2pi_engine {
       // the kernel left: wait for it to drain. An idle exit racing this request is
       // benign (serve it from a fresh launch with a fresh epoch); a hand-off timeout
       // (h_err set) is a device-side protocol fault and is reported, not retried
+      need_device();
       resident_stop();
       if (__atomic_load_n(h_err, __ATOMIC_ACQUIRE)) {
         __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
@@ -551,6 +583,7 @@ bool w4_eligible(const go2pi_engine &e, const go2pi::Model &m) {
   const int nl = (int)m.layers.size();
   if (!(e.opts.waves == 0 || e.opts.waves == 4) || nl < 2) return false;
   if (m.has_gru && m.gru.H % 64) return false;
+  if (m.has_gru && m.gru.cell == 0 && m.gru.lbr == 0) return false;  // the two-pass cell: generic body only
   if (std::getenv("GO2PI_NO_HEAD_FUSE") || std::getenv("GO2PI_NO_W4")) return false;  // env: A/B diagnostics only
   const int tpw = ceil64(m.layers[0].N) / 64, t_last = ceil16(m.layers[nl - 1].N) / 16;
   if (!(tpw == 2 || tpw == 4 || tpw == 8) || t_last > (tpw == 8 ? 1 : 2)) return false;
@@ -581,8 +614,10 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   if ((int)m.layers.size() > GO2PI_MAX_LAYERS)
     throw ApiError("policy has more than " + std::to_string(GO2PI_MAX_LAYERS) + " dense layers", GO2PI_E_MODEL);
   if (m.has_gru) {
-    if (m.gru.cell == 0 && m.gru.lbr != 1)
-      throw ApiError("GRU linear_before_reset=0 is not supported yet (export with lbr=1)", GO2PI_E_MODEL);
+    // lbr = 0 (Keras reset_after=False) runs the generic body's two-pass cell
+    // (fused_impl.hpp gru0_cell), one tile group per wave: H <= 256
+    if (m.gru.cell == 0 && m.gru.lbr == 0 && m.gru.H > 256)
+      throw ApiError("GRU linear_before_reset=0 with hidden size > 256 is not supported", GO2PI_E_MODEL);
     if (m.gru.H % 16) throw ApiError("recurrent hidden size must be a multiple of 16", GO2PI_E_MODEL);
   }
 
@@ -889,6 +924,24 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
 
 // Every C-ABI entry point runs through here: exceptions become status codes, and
 // the caller's current HIP device is restored on the way out.
+// (no DeviceRestore: go2pi_run's resident fast path, which switches devices lazily)
+template <class F>
+int guarded_nodev(F &&f) {
+  try {
+    g_last_error.clear();
+    return f();
+  } catch (const ApiError &ex) {
+    g_last_error = ex.what();
+    return ex.code;
+  } catch (const HipError &ex) {
+    g_last_error = ex.what();
+    return ex.code;
+  } catch (const std::exception &ex) {
+    g_last_error = ex.what();
+    return GO2PI_E_INVALID;
+  }
+}
+
 template <class F>
 int guarded(F &&f) {
   DeviceRestore keep;
@@ -1023,13 +1076,31 @@ int go2pi_io_dims(const go2pi_engine *e, int64_t *in_dim, int64_t *out_dim) {
 }
 
 int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
+  // batch <= 8 on a live resident kernel: served with no HIP runtime call (the device
+  // switch and its restore were three HIP API entries per act(), on the 5 us path)
+  bool res_try = true;
+  if (e && obs && act && batch >= 1 && batch <= GO2PI_SMALL_MAXB && batch <= e->opts.max_batch && e->resident_ok &&
+      e->resident_ready(nullptr)) {
+    e->lazy_dev = true;
+    const int rc = guarded_nodev([&] {
+      const bool ok = e->resident_serve(nullptr, obs, batch, 0u);
+      if (ok) {
+        e->check_handoff();
+        std::memcpy(act, e->h_act, sizeof(float) * (size_t)batch * e->model.out_dim);
+      }
+      return ok ? GO2PI_OK : 1;
+    });
+    e->dev_done();
+    if (rc != 1) return rc;
+    res_try = false;  // not served (evicted twice): a launch serves it
+  }
   return guarded([&] {
     check_engine(static_cast<const go2pi_engine *>(e));
     check_batch(e, batch);
     if (batch == 0) return GO2PI_OK;
     if (!obs || !act) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
-    if (e->resident_ok && batch <= GO2PI_SMALL_MAXB && e->resident_serve(nullptr, obs, batch, 0u)) {
+    if (res_try && e->resident_ok && batch <= GO2PI_SMALL_MAXB && e->resident_serve(nullptr, obs, batch, 0u)) {
       e->check_handoff();
       std::memcpy(act, e->h_act, sizeof(float) * (size_t)batch * e->model.out_dim);
       return GO2PI_OK;

@@ -513,9 +513,114 @@ __device__ __forceinline__ void gru_group(const DevGru &G, const float *X, const
   }
 }
 
+// GRU cell with linear_before_reset = 0 (ONNX GRU-14: n = tanh(Wh x + Wbh + Rh (r . h)
+// + Rbh); Keras reset_after=False) for one group of GT tiles. The reset gate must be
+// complete for every hidden unit before the n contraction over h can start, so the
+// cell runs in two passes over the [x | h] chunks with a workgroup barrier between:
+//   pass 1 (PH = 1): r over [x | h]; r . h written to Y (every wave reads it in pass 2);
+//   pass 2 (PH = 2): z over [x | h], n over [x | r . h]; h' = (1 - z) n + z h into hv.
+// Three gate contractions in all, as with lbr = 1. The caller stores hv to Y after a
+// second barrier (Y still holds r . h for the other waves until then).
+template <int GT, int PH>
+__device__ __forceinline__ void gru0_group(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                           int t_first, int lane, f32x4 (&hv)[GT]) {
+  const int Cx = G.I_pad >> 4, Ch = G.H >> 4, H = G.H;
+  const int col = lane & 15, r0 = (lane >> 4) << 2;
+  const WStream ws(G.w);
+  const int csb = Ch * 192 * 16;  // bytes per chunk: [chunk][tile][gate][lane]
+  int vo[GT];
+  f32x4 a0[GT], a1[GT];  // PH 1: r, -; PH 2: z, n
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+    vo[i] = ((t_first + i) * 192 + lane) * 16;
+    if (PH == 1) {
+      const float br = G.bzr[H + j];
+      a0[i] = f32x4{br, br, br, br};
+    } else {
+      const float bz = G.bzr[j], bn = G.bh[j] + G.bh[H + j];
+      a0[i] = f32x4{bz, bz, bz, bz};
+      a1[i] = f32x4{bn, bn, bn, bn};
+    }
+  }
+  const float *xrow = X + (lane & 15) * xs + ((lane >> 4) << 2);
+  const float *hrow = Hs + (lane & 15) * xs + ((lane >> 4) << 2);
+  const float *rrow = Y + (lane & 15) * xs + ((lane >> 4) << 2);
+  for (int c = 0; c < Cx + Ch; ++c) {
+    const bool xc = c < Cx;
+    const float4 a = xc ? *reinterpret_cast<const float4 *>(xrow + c * 16)
+                        : *reinterpret_cast<const float4 *>(hrow + (c - Cx) * 16);
+    float4 an = a;
+    if (PH == 2 && !xc) an = *reinterpret_cast<const float4 *>(rrow + (c - Cx) * 16);
+    float4 f0[GT], f1[GT];
+#pragma unroll
+    for (int i = 0; i < GT; ++i) {
+      f0[i] = ws.ld(vo[i] + (PH == 1 ? 1024 : 0), c * csb);  // r (PH 1) or z fragment
+      if (PH == 2) f1[i] = ws.ld(vo[i] + 2048, c * csb);     // n fragment (W_h on x, R_h on h)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < GT; ++i) {
+        a0[i] = mfma4(f4c(a, j), f4c(f0[i], j), a0[i]);
+        if (PH == 2) a1[i] = mfma4(f4c(an, j), f4c(f1[i], j), a1[i]);
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < GT; ++i) {
+    const int j = (t_first + i) * 16 + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r0 + e;
+      const float ho = Hs[row * xs + j];
+      if (PH == 1) {
+        Y[row * xs + j] = sigmoid_fast(a0[i][e]) * ho;
+      } else {
+        const float zg = sigmoid_fast(a0[i][e]);
+        const float hn = 2.f * sigmoid_fast(2.f * a1[i][e]) - 1.f;  // tanh, ~1e-7 abs
+        hv[i][e] = (1.f - zg) * hn + zg * ho;
+      }
+    }
+  }
+}
+
+// lbr = 0 over the workgroup: one group of <= GM tiles per wave (the engine admits
+// H <= 256 for lbr = 0, so tpw <= GM for every wave count); every wave passes both
+// barriers.
+template <int NW, int GM>
+__device__ __forceinline__ void gru0_cell(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
+                                          int wave, int lane) {
+  const int Ht = G.H >> 4;
+  const int tpw = (Ht + NW - 1) / NW;
+  const int t = wave * tpw, n = max(0, min(tpw, Ht - t));
+  f32x4 hv[GM];
+  auto pass = [&](auto ph) {
+    constexpr int PH = decltype(ph)::value;
+    if (n == GM) gru0_group<GM, PH>(G, X, Hs, Y, xs, t, lane, hv);
+    else if (GM >= 2 && n == 2) gru0_group<2, PH>(G, X, Hs, Y, xs, t, lane, reinterpret_cast<f32x4(&)[2]>(hv));
+    else if (n >= 1) {
+      for (int i = 0; i < n; ++i)
+        gru0_group<1, PH>(G, X, Hs, Y, xs, t + i, lane, reinterpret_cast<f32x4(&)[1]>(hv[i]));
+    }
+  };
+  pass(std::integral_constant<int, 1>{});
+  __syncthreads();  // r . h complete in Y
+  pass(std::integral_constant<int, 2>{});
+  __syncthreads();  // every wave done reading r . h
+  const int col = lane & 15, r0 = (lane >> 4) << 2;
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Y[(r0 + e) * xs + (t + i) * 16 + col] = hv[i][e];
+}
+
 template <int NW>
 __device__ __forceinline__ void gru_cell(const DevGru &G, const float *X, const float *Hs, float *Y, int xs,
                                          int wave, int lane) {
+  if (G.lbr == 0) {
+    constexpr int GM0 = NW >= 16 ? 1 : (NW >= 8 ? 2 : 4);
+    gru0_cell<NW, GM0>(G, X, Hs, Y, xs, wave, lane);
+    return;
+  }
   const int Ht = G.H >> 4;
   const int tpw = (Ht + NW - 1) / NW;
   int t = wave * tpw;

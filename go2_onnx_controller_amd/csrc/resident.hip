@@ -32,6 +32,7 @@
 // grid always drains. The host relaunches on its next request.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "ctl_fn.hpp"
@@ -1084,6 +1085,424 @@ __global__ __launch_bounds__(NT) void policy_resident1_kernel(const DevProgram *
   }
 }
 
+// ---------------------------------------------------------------------------
+// policy_act1_kernel — the one-workgroup resident act() of r05.
+// policy_resident1_kernel above gives every output its own group of 8 lanes: a
+// 128 x 128 layer then moves 1024 lanes x 64 B of its input row out of LDS (64 KB,
+// 256 LDS cycles at 256 B/clk) for 16K MACs, and 16 waves on 4 SIMDs serialise the
+// DPP trees: ~1.4K cycles per layer against ~130 of fma issue
+// (profiles/r04_res_timeline.json). Here:
+//
+//  * a dedicated polling wave (wave 0) and A1_CW = 8 compute waves (2 per SIMD);
+//  * a wide layer (N_pad = H, 64 or 128 outputs) gives each 16-lane DPP row R = H/32
+//    outputs: lane s of row g holds the weight float4s k = 64 f + 4 s .. +3 of the
+//    outputs 4g + r (R = 4), so one broadcast ds_read_b128 of the input feeds R
+//    output chains: 16 KB of LDS reads per 128 x 128 layer, a quarter of r04's;
+//  * the R partials are summed by a reduce-scatter over the row (row_ror:8, then
+//    row_half_mirror, then quad xor 2 and xor 1: five DPP adds for R = 4, no select),
+//    because lane s keeps its outputs in a rotated register order (a1_out);
+//  * the final layer (16 outputs, the head) runs on the first four compute waves,
+//    one output per DPP row, and its rows' first lanes store the answer granules;
+//  * the polling wave keeps D sweeps of the request granules in flight at once
+//    (a new sweep issued before the oldest is checked), so a request lands within
+//    one PCIe read round trip plus RTT / D instead of plus up to a whole RTT; it
+//    takes no part in the arithmetic, so its in-flight poll loads never sit in
+//    front of a compute wave's wait.
+// Summation order per output: two packed fma chains per register (x.xy, x.zw)
+// over the lane's float4s, their sum, then the fixed DPP tree: deterministic,
+// within the 1e-5 contract of the fp64 oracle (not the MFMA path's order).
+constexpr int A1_CW = 8;                 // compute waves
+constexpr int A1_NT = 64 * (1 + A1_CW);  // + the polling wave
+constexpr int A1_NP = 2;                 // granule loads per lane per sweep (header + <= 127 obs floats)
+
+// the weight register of output r ... : lane s of a row keeps output
+// r(j, s) = j ^ 2 [s >= 8] ^ [(s >> 2) & 1] in register j (R = 4), j ^ [s >= 8] (R = 2),
+// so that every step of the reduce-scatter adds the same register index of its partner
+template <int R>
+__device__ __forceinline__ int a1_out(int j, int s) {
+  if constexpr (R == 4) return j ^ ((s >> 3) << 1) ^ ((s >> 2) & 1);
+  else if constexpr (R == 2) return j ^ (s >> 3);
+  else return 0;
+}
+// after the reduce-scatter lane s holds the row's output a1_fin(s) (R = 4: its quad)
+template <int R>
+__device__ __forceinline__ int a1_fin(int s) {
+  if constexpr (R == 4) return s >> 2;
+  else if constexpr (R == 2) return s >> 3;
+  else return 0;
+}
+
+template <int R>
+__device__ __forceinline__ float a1_reduce(float (&p)[R]) {
+  if constexpr (R == 4) {
+    p[0] += dpp_f<0x128>(p[2]);  // row_ror:8 (lane s ^ 8): the partner keeps the other pair
+    p[1] += dpp_f<0x128>(p[3]);
+    p[0] += dpp_f<0x141>(p[1]);  // row_half_mirror (s ^ 7 within 8)
+  } else if constexpr (R == 2) {
+    p[0] += dpp_f<0x128>(p[1]);
+    p[0] += dpp_f<0x141>(p[0]);
+  } else {
+    p[0] += dpp_f<0x128>(p[0]);
+    p[0] += dpp_f<0x141>(p[0]);
+  }
+  p[0] += dpp_f<0x4E>(p[0]);  // quad_perm [2, 3, 0, 1]
+  p[0] += dpp_f<0xB1>(p[0]);  // quad_perm [1, 0, 3, 2]
+  return p[0];
+}
+
+// One sweep's granule i of the request (i = u * 64 + lane; 0 = header) into layer 0's
+// input rows: flat observation index i - 1 -> row b, column k (x0 stride S).
+__device__ __forceinline__ void a1_put(float *x0, int S, int in_dim, int B, int i, float v) {
+  const int f = i - 1;
+  const int b = B == 1 ? 0 : f / in_dim;
+  x0[b * S + (f - b * in_dim)] = v;
+}
+
+// The polling wave's wait for the next request. D sweeps of the header and the
+// observation granules in flight (pinned host memory, system scope), each checked when
+// it lands; the yield counter rides along with every sweep. 1: a request, its
+// observation rows (through the prologue) in x0; 0: leave (LEAVE header, idle bound,
+// moved yield counter, or a sweep that met a LEAVE granule). yield is never null (a
+// zero word stands in): a conditional load in the ring made the compiler wait for
+// every sweep in flight. v / yv: the sweep registers, owned by the caller and live
+// across its whole request loop, so that after a request is seen the sweeps still in
+// flight keep their registers: reused for the request word, the compiler made the
+// poller wait for them (~a PCIe round trip) before the staging barrier.
+template <int D, bool PRO>
+__device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned last, u64 idle_ticks, float *x0,
+                                       unsigned *err, int lane, unsigned &e, int &B, const unsigned *yield,
+                                       unsigned y0, const Pro &pro, const ProK (&pk)[A1_NP], u64 (&v)[D][A1_NP],
+                                       unsigned (&yv)[D]) {
+  u64 *qm = const_cast<u64 *>(q);
+  const int npoll = min(1 + in_dim, 64 * A1_NP);
+  // the previous call's sweeps, landed long ago: used here, so their registers stay
+  // theirs until now
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    asm volatile("" ::"v"(yv[d]));
+#pragma unroll
+    for (int u = 0; u < A1_NP; ++u) asm volatile("" ::"v"(v[d][u]));
+  }
+  auto issue = [&](int d) {
+#pragma unroll
+    for (int u = 0; u < A1_NP; ++u)
+      v[d][u] = __hip_atomic_load(qm + min(u * 64 + lane, npoll - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    yv[d] = __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+#pragma unroll
+  for (int d = 0; d + 1 < D; ++d) issue(d);
+  const u64 t0 = wall_clock64();
+  for (;;) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      issue((d + D - 1) % D);  // the newest sweep, before the oldest is looked at
+      if (__builtin_amdgcn_readfirstlane(yv[d]) != y0) return 0;
+      const unsigned tag = __builtin_amdgcn_readfirstlane((unsigned)(v[d][0] >> 32));
+      if (tag == GO2PI_RES_LEAVE) return 0;
+      if (tag != 0u && tag != last) {
+        const unsigned word = __builtin_amdgcn_readfirstlane((unsigned)v[d][0]);
+        B = min(max((int)(word & 0xFFu), 1), GO2PI_SMALL_MAXB);
+        const int n = B * in_dim;
+        if (1 + n <= npoll) {
+          bool ok = true;
+#pragma unroll
+          for (int u = 0; u < A1_NP; ++u) {
+            const int i = u * 64 + lane;
+            if (i >= 1 && i <= n) ok &= (unsigned)(v[d][u] >> 32) == tag;
+          }
+          if (__all(ok)) {
+#pragma unroll
+            for (int u = 0; u < A1_NP; ++u) {
+              const int i = u * 64 + lane;
+              if (i >= 1 && i <= n) {
+                const float x = __uint_as_float((unsigned)v[d][u]);
+                a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, pk[u], x) : x);
+              }
+            }
+            e = tag;
+            return 1;
+          }
+        } else {  // more granules than one sweep holds (B > 1 with a wide observation)
+          e = tag;
+          for (unsigned spins = 0;; ++spins) {
+            bool ok = true, lv = false;
+            for (int i = 1 + lane; i <= n; i += 64) {
+              const u64 g = __hip_atomic_load(qm + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              const unsigned t = (unsigned)(g >> 32);
+              ok &= t == tag;
+              lv |= t == GO2PI_RES_LEAVE;
+              const int k = (i - 1) % in_dim;
+              const float x = __uint_as_float((unsigned)g);
+              a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, x, k) : x);
+            }
+            if (__any(lv)) return 0;
+            if (__all(ok)) return 1;
+            if (spins > (1u << 22)) {
+              if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              return 0;
+            }
+          }
+        }
+      }
+      if (wall_clock64() - t0 > idle_ticks) return 0;
+    }
+  }
+}
+
+// A1_STAMP: RESCLK diagnostics, wall clock (slot i) / shader clock (A1_CLOCK) of the
+// first compute lane (tid 64) or, for the poll marks, of the polling wave (tid 0).
+#ifdef GO2PI_DIAG_RESCLK
+#define A1_STAMP(t, i)                                                                           \
+  do {                                                                                           \
+    if (P.stamps && tid == (t)) P.stamps[(size_t)(nreq & 511) * 32 + (i)] = wall_clock64();      \
+  } while (0)
+#define A1_CLOCK(t, i)                                                                                        \
+  do {                                                                                                        \
+    if (P.stamps && tid == (t)) P.stamps[(size_t)(nreq & 511) * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define A1_STAMP(t, i) \
+  do {                 \
+  } while (0)
+#define A1_CLOCK(t, i) \
+  do {                 \
+  } while (0)
+#endif
+
+// NL: dense layers (2..4): NL - 1 wide layers of H outputs (H = 64 or 128), then the
+// 16-output head. F0: layer 0's float4s per lane (K0_pad <= 64 F0). AS: the layers'
+// activation kinds, 4 bits each (layer l at 4l; the shipped model: 0x0111), or
+// 0xFFFFFFFF: read at run time. D: poll sweeps in flight. PRO: the program has an
+// observation prologue (Sub / Div / Mul / Clip), applied by the polling wave.
+template <int NL, int H, int F0, unsigned AS, int D, bool PRO>
+__global__ __launch_bounds__(A1_NT) void policy_act1_kernel(const DevProgram *__restrict__ Pd, const u64 *req,
+                                                            u64 *actg, unsigned *err, unsigned *done,
+                                                            u64 idle_ticks, const unsigned *yield) {
+  static_assert(NL >= 2 && NL <= 4 && (H == 64 || H == 128) && F0 >= 1 && F0 <= 4, "policy_act1_kernel shape");
+  constexpr int R = H / 32;   // outputs per lane in a wide layer
+  constexpr int HF = H / 64;  // float4s per lane of a K = H layer
+  constexpr int NM = NL - 2 > 0 ? NL - 2 : 1;  // wide layers after layer 0 (array extent)
+  const DevProgram &P = *Pd;
+  extern __shared__ float4 lds4[];
+  const int S = P.lds_stride;
+  float *x0 = reinterpret_cast<float *>(lds4);  // [8][S] layer 0's input rows (zero past in_dim)
+  float *xa = x0 + GO2PI_SMALL_MAXB * S;        // [8][S] wide layers' rows (ping-pong)
+  float *xb = xa + GO2PI_SMALL_MAXB * S;
+  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = tid - 64;                // compute lane (the polling wave: negative)
+  const int s = c & 15, grp = c >> 4;    // k-slice within the DPP row, the row
+  const int in_dim = P.in_dim, nout = P.out_dim;
+  // ---- weights in registers for the kernel's life (zero where k >= K_pad)
+  float4 w0[F0][R], wm[NM][HF][R], wo[HF];
+  float bw[NL - 1], bo = 0.f;
+  auto wld = [&](const DevLayer &L, int n, int k) {
+    const int T = L.N_pad >> 4;
+    const float4 *W = reinterpret_cast<const float4 *>(L.w);
+    return k < L.K_pad ? W[((size_t)(k >> 4) * T + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2)]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int l = 0; l < NL - 1; ++l) {
+    bw[l] = 0.f;
+    const DevLayer &L = P.L[l];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int n = R * grp + a1_out<R>(j, s);
+      if (l == 0) {
+#pragma unroll
+        for (int f = 0; f < F0; ++f) w0[f][j] = c >= 0 ? wld(L, n, 64 * f + 4 * s) : z4;
+      } else {
+#pragma unroll
+        for (int f = 0; f < HF; ++f) wm[l - 1][f][j] = c >= 0 ? wld(L, n, 64 * f + 4 * s) : z4;
+      }
+    }
+    if (c >= 0) bw[l] = L.bias[R * grp + a1_fin<R>(s)];
+  }
+  if constexpr (NL == 2) {
+#pragma unroll
+    for (int f = 0; f < HF; ++f)
+#pragma unroll
+      for (int j = 0; j < R; ++j) wm[0][f][j] = z4;
+  }
+  {
+    const DevLayer &L = P.L[NL - 1];
+    const bool hl = c >= 0 && c < 256;
+#pragma unroll
+    for (int f = 0; f < HF; ++f) wo[f] = hl ? wld(L, grp, 64 * f + 4 * s) : z4;
+    if (hl) bo = L.bias[grp];
+  }
+  // the program fields a request reads, in SGPRs for the kernel's life
+  int lact[NL];
+  float lal[NL], lbe[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    lact[l] = r1_keep(P.L[l].act);
+    lal[l] = r1_keep(P.L[l].alpha);
+    lbe[l] = r1_keep(P.L[l].beta);
+  }
+  const int post_tanh = r1_keep(P.post_tanh);
+  const float clo = r1_keep(P.clip_lo), chi = r1_keep(P.clip_hi), pscale = r1_keep(P.scale);
+  // the polling wave: each lane's prologue constants for its granule positions (the
+  // column of granule i is (i - 1) mod in_dim whatever the batch)
+  const Pro pro = PRO ? pro_of(P) : Pro{};
+  ProK pk[A1_NP];
+#pragma unroll
+  for (int u = 0; u < A1_NP; ++u) {
+    const int i = u * 64 + lane;
+    pk[u] = (PRO && wave == 0 && i >= 1) ? pro_k(pro, (i - 1) % in_dim) : ProK{0.f, 1.f, 1.f};
+  }
+  for (int i = tid; i < GO2PI_SMALL_MAXB * S; i += A1_NT) x0[i] = 0.f;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): weights and constants in registers before the first wait
+  const unsigned y0 = __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();  // x0 cleared before the poller writes a row into it
+  unsigned last = 0, nreq = 0;
+  (void)nreq;
+  u64 pv[D][A1_NP];  // the polling wave's sweep registers (a1_poll)
+  unsigned pyv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    pyv[d] = 0u;
+#pragma unroll
+    for (int u = 0; u < A1_NP; ++u) pv[d][u] = 0ull;
+  }
+  for (;;) {
+    if (wave == 0) {
+      unsigned e = 0;
+      int B = 1;
+      const int got =
+          a1_poll<D, PRO>(req, in_dim, S, last, idle_ticks, x0, err, lane, e, B, yield, y0, pro, pk, pv, pyv);
+      A1_STAMP(0, 0);
+      A1_CLOCK(0, 15);
+      if (lane == 0) {
+        st[0] = !got;
+        st[1] = (int)e;
+        st[2] = B;
+      }
+    }
+    lds_barrier();  // the request's rows are in x0
+    // (row 0's layer-0 input read beside the request word: one LDS round trip, not two)
+    float4 xpre[F0];
+#pragma unroll
+    for (int f = 0; f < F0; ++f) xpre[f] = *reinterpret_cast<const float4 *>(x0 + 64 * f + 4 * s);
+    const int4 sv = *reinterpret_cast<const int4 *>(st);
+    if (sv.x) break;
+    const unsigned e = (unsigned)sv.y;
+    const int B = sv.z;
+    last = e;
+    if (wave == 0) {  // the poller passes the layers' barriers, then polls again
+#pragma unroll
+      for (int l = 0; l + 1 < NL; ++l) lds_barrier();
+      ++nreq;
+      continue;
+    }
+    A1_STAMP(64, 1);
+    A1_CLOCK(64, 13);
+    // ---- wide layers
+    float *X = x0, *Y = xa;
+#pragma unroll
+    for (int l = 0; l < NL - 1; ++l) {
+      const int A = AS != 0xFFFFFFFFu ? (int)((AS >> (4 * l)) & 15u) : lact[l];
+      for (int b = 0; b < B; ++b) {
+        f32x2 acc[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[j] = f32x2{0.f, 0.f};
+        const float *xr = X + b * S + 4 * s;
+        if (l == 0) {
+#pragma unroll
+          for (int f = 0; f < F0; ++f) {
+            const float4 x = b == 0 ? xpre[f] : *reinterpret_cast<const float4 *>(xr + 64 * f);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+              acc[j] = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{w0[f][j].x, w0[f][j].y}, acc[j]);
+              acc[j] = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{w0[f][j].z, w0[f][j].w}, acc[j]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int f = 0; f < HF; ++f) {
+            const float4 x = *reinterpret_cast<const float4 *>(xr + 64 * f);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+              const float4 wv = wm[l > 0 ? l - 1 : 0][f][j];
+              acc[j] = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{wv.x, wv.y}, acc[j]);
+              acc[j] = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{wv.z, wv.w}, acc[j]);
+            }
+          }
+        }
+        if (l == 0 && b == 0) A1_CLOCK(64, 16);
+        float p[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) p[j] = acc[j].x + acc[j].y;
+        const float v = a1_reduce<R>(p);
+        if (l == 0 && b == 0) A1_CLOCK(64, 17);
+        if ((s & (16 / R - 1)) == 0) Y[b * S + R * grp + a1_fin<R>(s)] = act_fn(A, lal[l], lbe[l], v + bw[l]);
+      }
+      if (l == 0) A1_CLOCK(64, 18);
+      lds_barrier();
+      if (l < 6) A1_STAMP(64, 2 + l);
+      if (l < 3) A1_CLOCK(64, 25 + l);
+      X = Y;
+      Y = Y == xa ? xb : xa;
+    }
+    // ---- the head: 16 outputs, one per DPP row of compute waves 0..3
+    if (c < 256) {
+      const int A = AS != 0xFFFFFFFFu ? (int)((AS >> (4 * (NL - 1))) & 15u) : lact[NL - 1];
+      for (int b = 0; b < B; ++b) {
+        f32x2 acc = {0.f, 0.f};
+        const float *xr = X + b * S + 4 * s;
+#pragma unroll
+        for (int f = 0; f < HF; ++f) {
+          const float4 x = *reinterpret_cast<const float4 *>(xr + 64 * f);
+          acc = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{wo[f].x, wo[f].y}, acc);
+          acc = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{wo[f].z, wo[f].w}, acc);
+        }
+        float p[1] = {acc.x + acc.y};
+        const float v = a1_reduce<1>(p);
+        if (s == 0 && grp < nout) {
+          float y = act_fn(A, lal[NL - 1], lbe[NL - 1], v + bo);
+          if (post_tanh) y = tanhf(y);
+          y = clip_nan(y, clo, chi) * pscale;
+          __hip_atomic_store(actg + (size_t)b * nout + grp, ((u64)e << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+    A1_STAMP(64, 8);
+    A1_CLOCK(64, 14);
+    ++nreq;
+  }
+  // leaving: every wave's answer stores (and the poller's sweeps) drained before the
+  // LEAVE done word, so a host that sees LEAVE and rescans finds a served request's
+  // granules (engine.cpp resident_serve)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the act1 shape of program p: {NL, H, F0}, or NL = 0 when it does not apply
+struct A1Shape {
+  int nl, h, f0;
+};
+A1Shape act1_shape(const DevProgram &p) {
+  A1Shape a{0, 0, 0};
+  if (p.has_gru || p.nl < 2 || p.nl > 4 || p.L[p.nl - 1].N_pad != 16) return a;
+  const int H = p.L[0].N_pad;
+  if (H != 64 && H != 128) return a;
+  for (int l = 1; l < p.nl; ++l)
+    if (p.L[l].K_pad != H || (l + 1 < p.nl && p.L[l].N_pad != H)) return a;
+  int f0 = (p.L[0].K_pad + 63) / 64;
+  if (f0 == 3) f0 = 4;
+  // (layer 0's lanes read their input row up to 64 F0: inside the row, zero past in_dim)
+  if (f0 > 4 || p.lds_stride < std::max(64 * f0, H)) return a;
+  a.nl = p.nl;
+  a.h = H;
+  a.f0 = f0;
+  return a;
+}
+
 size_t resident1_lds_bytes(const DevProgram &p, bool ctl) {
   size_t f = 3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 + ((size_t)GO2PI_SMALL_MAXB * p.in_dim + 3) / 4 * 4;
   if (ctl) f += (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) + (size_t)GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + p.in_dim);
@@ -1114,6 +1533,31 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
     if (p.nl == 4 && elu1 && r1_shape(p, 512) == 0x2887u && r1_lgs(p, 512) == 0x4222u)
       return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x2887u, 0x4222u, 0x0111u>, 512);
     return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x8888u>, 512);
+  }
+  // r05: the polling-wave form (policy_act1_kernel) wherever its shape applies
+  // (GO2PI_RES_R1W=1: the r04 1024-thread form, A/B diagnostics; GO2PI_A1_DEPTH: poll
+  // sweeps in flight, 1 / 2 / 4)
+  const A1Shape a1 = act1_shape(p);
+  if (a1.nl && !std::getenv("GO2PI_RES_R1W")) {
+    const size_t lds1 = sizeof(float) * (3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4);
+    auto go1 = [&](auto kern) {
+      if (lds1 > 64 * 1024) {
+        const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+        if (a != hipSuccess) return (int)a;
+      }
+      // (yield never null: the kernel loads it unconditionally, see a1_poll)
+      hipLaunchKernelGGL(kern, dim3(1), dim3(A1_NT), lds1, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
+                         err, done, idle_ticks, yield ? yield : reinterpret_cast<const unsigned *>(p.zero));
+      return (int)hipGetLastError();
+    };
+    const char *dv = std::getenv("GO2PI_A1_DEPTH");
+    const int depth = dv ? std::atoi(dv) : 2;
+    const bool pro = p.pre_sub || p.pre_div || p.pre_mul || p.pre_clip;
+    if (a1.nl == 4 && a1.h == 128 && a1.f0 == 2 && elu1 && !pro) {
+      if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false>);
+      return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 2, false>);
+    }
   }
   if (p.nl == 4 && elu1 && r1_shape(p, 1024) == 0x2444u && r1_lgs(p, 1024) == 0x4333u)
     return go(policy_resident1_kernel<1024, R1_LMAX, 4, false, 0x2444u, 0x4333u, 0x0111u>, 1024);

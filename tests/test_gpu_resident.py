@@ -26,16 +26,23 @@ def _models(synth_path):
 
 
 # resident forms: "one" the single-workgroup kernel (the default where the weights fit
-# one CU: the shipped model), "multi" the multi-workgroup kernel (GO2PI_RES_MULTI=1 for
-# the shipped model; the only form for mlp512), "tiled0" multi with layer 0 tiled like
-# every other layer (bit-identical to the launch path)
-@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "multi"), ("shipped", "tiled0"),
+# one CU: the shipped model; r05 policy_act1_kernel, a polling wave + 8 compute waves,
+# two poll sweeps in flight), "one_d1" the same with one sweep in flight, "one_r1w" the
+# r04 1024-thread form (GO2PI_RES_R1W=1), "multi" the multi-workgroup kernel
+# (GO2PI_RES_MULTI=1 for the shipped model; the only form for mlp512), "tiled0" multi
+# with layer 0 tiled like every other layer (bit-identical to the launch path)
+@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "one_d1"), ("shipped", "one_r1w"),
+                                       ("shipped", "multi"), ("shipped", "tiled0"),
                                        ("mlp512", "multi"), ("mlp512", "tiled0")])
 def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import mlp_ref
     tiled0 = form == "tiled0"
-    if form != "one":
+    if form == "one_d1":
+        monkeypatch.setenv("GO2PI_A1_DEPTH", "1")  # read at each resident launch
+    elif form == "one_r1w":
+        monkeypatch.setenv("GO2PI_RES_R1W", "1")
+    elif form != "one":
         monkeypatch.setenv("GO2PI_RES_MULTI", "1")  # read at engine creation
     if tiled0:
         monkeypatch.setenv("GO2PI_RES_TILED0", "1")  # read at each resident launch

@@ -1,0 +1,32 @@
+#!/bin/bash
+# r05 batch-1 latency A/B on the GPU box: the drop-in ONNXActor::act() timed from C++
+# (as the reference's main.cpp:38-42 times it) for the shipped model, alternating the
+# r05 one-workgroup kernel (policy_act1_kernel: polling wave + 8 compute waves, two poll
+# sweeps in flight; default), the same with one sweep (GO2PI_A1_DEPTH=1), the r04
+# 1024-thread form (GO2PI_RES_R1W=1) and a launch per call (GO2PI_RESIDENT_MS=0);
+# then, with a resclk build present, the request timeline (tools/res_timeline.py).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/lat
+mkdir -p $O $R/build
+L=$R/go2_onnx_controller_amd/lib
+g++ -std=c++20 -O2 -I$R/include $R/tests/cpp/controller_shape.cpp -L$L -lonnx_actor -Wl,-rpath,$L -o $R/build/controller_shape || exit 1
+M=$R/tests/golden/model.onnx
+for round in 1 2 3; do
+  for v in a1d2 a1d1 r1w launch; do
+    case $v in
+      a1d2) env="" ;;
+      a1d1) env="GO2PI_A1_DEPTH=1" ;;
+      r1w) env="GO2PI_RES_R1W=1" ;;
+      launch) env="GO2PI_RESIDENT_MS=0" ;;
+    esac
+    r=$(env $env timeout -k 10 60 $R/build/controller_shape $M lat 10000 1000 98 12) || { echo "lat $v failed: $r"; exit 1; }
+    echo "round $round $v $(echo $r | tr '\n' ' ')" | tee -a $O/ab.txt
+  done
+done
+if [ -f $L/diag/libgo2pi_resclk.so ]; then
+  GO2PI_LIB=$L/diag/libgo2pi_resclk.so timeout -k 10 120 python3 $R/tools/res_timeline.py --model shipped --form one \
+    --out $O/res_timeline_one.json > $O/res_timeline.log 2>&1 || { echo "timeline failed"; tail -20 $O/res_timeline.log; exit 1; }
+  tail -30 $O/res_timeline_one.json
+fi
+echo "r05_latency ok"
