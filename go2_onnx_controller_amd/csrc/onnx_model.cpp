@@ -14,7 +14,9 @@
 // shipped model at byte 730), so every payload is memcpy'd, never aliased.
 #include "onnx_model.hpp"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -298,6 +300,204 @@ void act_attrs(const Node &nd, int act, float &alpha, float &beta) {
   }
 }
 
+// An int64 vector input of a node (Slice starts / ends / axes / steps), or empty.
+std::vector<int64_t> ints_of(const std::unordered_map<std::string, Tensor> &inits, const Node &nd, size_t k) {
+  if (nd.in.size() <= k || nd.in[k].empty()) return {};
+  auto it = inits.find(nd.in[k]);
+  if (it == inits.end() || it->second.dtype != 7) fail(nd.op + ": input " + std::to_string(k) + " must be an INT64 constant");
+  return it->second.i;
+}
+
+// The per-block observation front-end: the observation Sliced into column blocks,
+// each block through its own Sub / Div / Mul / Clip, then Concatenated on the feature
+// axis (e.g. per-block normalisation of a controller's history blocks, controller.hpp
+// :45-68). When the blocks cover the observation's columns in order, the front-end is
+// exactly a per-column prologue: (x - sub[k]) / div[k] * mul[k], clipped, with each
+// block's constants at its columns and the identity where a block has no such op. The
+// blocks' Clip bounds must agree (the prologue clip is one interval). The walk then
+// starts at the Concat's output; a graph with no Slice on the observation is left as it
+// is. (The reference hands any graph to onnxruntime, onnx_actor.cpp:16; a front-end
+// this cannot lower exactly is refused, never approximated.)
+void front_end(Model &m, const std::vector<Node> &nodes, const std::unordered_map<std::string, Tensor> &inits,
+               const std::unordered_map<std::string, std::vector<size_t>> &consumers, std::vector<bool> &used,
+               std::string &cur) {
+  const std::string obs = m.inputs[0].name;
+  auto ci = consumers.find(obs);
+  if (ci == consumers.end()) return;
+  bool any_slice = false;
+  for (size_t k : ci->second) any_slice |= nodes[k].op == "Slice";
+  if (!any_slice) return;
+  const auto &shape = m.inputs[0].shape;
+  if (shape.size() != 2 || shape[1] <= 0) fail("Slice on the observation needs a static [batch, features] input shape");
+  const int64_t F = shape[1];
+  auto only_consumer = [&](const std::string &v) -> size_t {
+    auto it = consumers.find(v);
+    if (it == consumers.end() || it->second.size() != 1) fail("front-end value '" + v + "' must have exactly one consumer");
+    return it->second[0];
+  };
+  auto fconst = [&](const Node &nd, const std::string &x) -> const Tensor & {
+    const std::string &o = nd.in.at(0) == x ? nd.in.at(1) : nd.in.at(0);
+    auto it = inits.find(o);
+    if (it == inits.end() || it->second.dtype != 1) fail(nd.op + " in the observation front-end needs a FLOAT constant");
+    if (nd.op == "Div" && nd.in.at(0) != x) fail("Div in the observation front-end must divide the observation");
+    return it->second;
+  };
+  struct Block {
+    int64_t b = 0, e = 0;
+    std::vector<float> sub, div, mul;
+    float lo = -INFINITY, hi = INFINITY;
+    bool clip = false;
+    std::string tail;
+  };
+  std::vector<Block> blocks;
+  size_t concat = SIZE_MAX;
+  for (size_t k : ci->second) {
+    const Node &sl = nodes[k];
+    if (sl.op != "Slice" || sl.in.at(0) != obs) fail("the observation feeds a Slice front-end and a '" + sl.op + "'");
+    std::vector<int64_t> st, en, ax, sp;
+    if (sl.in.size() > 1) {
+      st = ints_of(inits, sl, 1);
+      en = ints_of(inits, sl, 2);
+      ax = ints_of(inits, sl, 3);
+      sp = ints_of(inits, sl, 4);
+    } else {  // opset 1-9: attributes
+      auto a = sl.attrs.find("starts"), b = sl.attrs.find("ends"), c = sl.attrs.find("axes");
+      if (a == sl.attrs.end() || b == sl.attrs.end()) fail("Slice without starts / ends");
+      st = a->second.ints;
+      en = b->second.ints;
+      if (c != sl.attrs.end()) ax = c->second.ints;
+    }
+    if (ax.empty())
+      for (size_t i = 0; i < st.size(); ++i) ax.push_back((int64_t)i);
+    if (st.size() != en.size() || ax.size() != st.size() || (!sp.empty() && sp.size() != st.size()))
+      fail("Slice: starts / ends / axes / steps lengths differ");
+    Block bl;
+    bl.b = 0;
+    bl.e = F;
+    for (size_t i = 0; i < st.size(); ++i) {
+      const int64_t a = ax[i] < 0 ? ax[i] + 2 : ax[i];
+      if (!sp.empty() && sp[i] != 1) fail("Slice with a step other than 1 is unsupported");
+      auto clampi = [&](int64_t v, int64_t dim) { return std::max<int64_t>(0, std::min(v < 0 ? v + dim : v, dim)); };
+      if (a == 0) {
+        if (clampi(st[i], INT64_MAX) != 0 || en[i] < INT32_MAX) fail("Slice on the batch axis is unsupported");
+      } else if (a == 1) {
+        bl.b = clampi(st[i], F);
+        bl.e = clampi(en[i], F);
+      } else {
+        fail("Slice axis out of range for a [batch, features] observation");
+      }
+    }
+    if (bl.e <= bl.b) fail("empty Slice of the observation");
+    used[k] = true;
+    const int64_t w = bl.e - bl.b;
+    auto per_col = [&](const Tensor &C, const std::string &what) {
+      if (C.numel() != 1 && C.numel() != w) fail(what + " in the front-end must broadcast over its block's " +
+                                                 std::to_string(w) + " columns");
+      std::vector<float> v((size_t)w);
+      for (int64_t j = 0; j < w; ++j) v[(size_t)j] = C.numel() == 1 ? C.f.at(0) : C.f.at((size_t)j);
+      return v;
+    };
+    // the block's chain: Sub?, Div? / Mul?, Clip?, Identity anywhere, then the Concat
+    std::string x = sl.out.at(0);
+    for (int hop = 0; hop < 16; ++hop) {
+      const size_t n = only_consumer(x);
+      const Node &nd = nodes[n];
+      if (nd.op == "Concat") {
+        if (concat != SIZE_MAX && concat != n) fail("the observation's Slices feed different Concats");
+        concat = n;
+        break;
+      }
+      used[n] = true;
+      if (nd.op == "Identity") {
+      } else if (nd.op == "Sub") {
+        if (!bl.sub.empty() || !bl.div.empty() || !bl.mul.empty() || bl.clip) fail("front-end block: Sub must come first");
+        bl.sub = per_col(fconst(nd, x), "Sub");
+      } else if (nd.op == "Div") {
+        if (!bl.div.empty() || !bl.mul.empty() || bl.clip) fail("front-end block must be Sub, Div, Mul, then Clip");
+        bl.div = per_col(fconst(nd, x), "Div");
+      } else if (nd.op == "Mul") {
+        if (!bl.mul.empty() || bl.clip) fail("front-end block must be Sub, Div, Mul, then Clip");
+        bl.mul = per_col(fconst(nd, x), "Mul");
+      } else if (nd.op == "Clip") {
+        if (bl.clip) fail("front-end block: two Clips");
+        bl.lo = nd.fattr("min", -INFINITY);
+        bl.hi = nd.fattr("max", INFINITY);
+        auto sc = [&](size_t k2, float &v) {
+          if (nd.in.size() > k2 && !nd.in[k2].empty()) {
+            auto it = inits.find(nd.in[k2]);
+            if (it == inits.end() || it->second.dtype != 1 || it->second.numel() != 1 || it->second.f.empty())
+              fail("front-end Clip bounds must be FLOAT scalars");
+            v = it->second.f[0];
+          }
+        };
+        sc(1, bl.lo);
+        sc(2, bl.hi);
+        bl.clip = true;
+      } else {
+        fail("unsupported operator '" + nd.op + "' in the observation front-end (node '" + nd.name + "')");
+      }
+      if (nd.out.empty()) fail("node without output");
+      x = nd.out[0];
+    }
+    if (concat == SIZE_MAX) fail("the observation's Slice chain does not reach a Concat");
+    bl.tail = x;
+    blocks.push_back(std::move(bl));
+  }
+  const Node &cc = nodes[concat];
+  const int64_t axis = cc.iattr("axis", 1);
+  if (axis != 1 && axis != -1) fail("Concat of the observation blocks must be on the feature axis");
+  if (cc.in.size() != blocks.size()) fail("the Concat after the observation Slices takes other inputs too");
+  // the blocks in Concat order must cover [0, F) in order
+  std::vector<Block *> order;
+  for (const auto &name : cc.in) {
+    Block *hit = nullptr;
+    for (auto &bl : blocks)
+      if (bl.tail == name && !hit) hit = &bl;
+    if (!hit) fail("Concat input '" + name + "' is not an observation block");
+    order.push_back(hit);
+  }
+  int64_t at = 0;
+  for (Block *bl : order) {
+    if (bl->b != at) fail("the observation blocks must cover its columns in order (a reordering front-end is unsupported)");
+    at = bl->e;
+  }
+  if (at != F) fail("the observation blocks must cover all of its columns");
+  bool any_sub = false, any_div = false, any_mul = false, any_clip = false;
+  float lo = -INFINITY, hi = INFINITY;
+  for (Block *bl : order) {
+    any_sub |= !bl->sub.empty();
+    any_div |= !bl->div.empty();
+    any_mul |= !bl->mul.empty();
+    if (bl->clip) {
+      if (any_clip && (bl->lo != lo || bl->hi != hi)) fail("the observation blocks' Clip bounds differ");
+      any_clip = true;
+      lo = bl->lo;
+      hi = bl->hi;
+    }
+  }
+  if (any_clip)
+    for (Block *bl : order)
+      if (!bl->clip) fail("only some observation blocks are clipped");
+  auto cat = [&](bool any, std::vector<float> Block::*f, float ident, std::vector<float> &dst) {
+    if (!any) return;
+    dst.clear();
+    for (Block *bl : order) {
+      const auto &v = bl->*f;
+      if (v.empty()) dst.insert(dst.end(), (size_t)(bl->e - bl->b), ident);
+      else dst.insert(dst.end(), v.begin(), v.end());
+    }
+  };
+  cat(any_sub, &Block::sub, 0.f, m.pre_sub);
+  cat(any_div, &Block::div, 1.f, m.pre_div);
+  cat(any_mul, &Block::mul, 1.f, m.pre_mul);
+  if (any_clip) {
+    m.pre_lo = lo;
+    m.pre_hi = hi;
+  }
+  used[concat] = true;
+  cur = cc.out.at(0);
+}
+
 }  // namespace
 
 Model parse_onnx(const uint8_t *data, size_t n) {
@@ -373,6 +573,7 @@ Model parse_onnx(const uint8_t *data, size_t n) {
   // Walk the single-consumer chain from input 0 to output 0.
   std::string cur = m.inputs[0].name;
   std::vector<bool> used(nodes.size(), false);
+  front_end(m, nodes, inits, consumers, used, cur);
   bool last_has_act = true;  // true => next Add cannot fold into a bias
   bool pending_bias_ok = false;
   // elementwise ops after the last layer's activation: a Mul by a constant is held

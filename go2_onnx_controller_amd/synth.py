@@ -90,7 +90,9 @@ def gru_params(I=48, H=256, seed=0):
     return W, R, B
 
 
-def gru_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch") -> bytes:
+def gru_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch", lbr=1) -> bytes:
+    """lbr: linear_before_reset (1: torch.onnx.export's nn.GRU and Keras' default
+    reset_after=True; 0: Keras reset_after=False and the ONNX default)."""
     W, R, B = gru_params(I, H, seed)
     layers = mlp_layers((H,) + tuple(head), seed, first_tid=200)
     axes = np.array([0], np.int64)
@@ -98,7 +100,7 @@ def gru_model_bytes(I=48, H=256, head=(512, 512, 512, 12), seed=0, batch="batch"
     nodes = [
         ow.node("Unsqueeze", ["observation", "axes0"], ["x_seq"], "/gru/Unsqueeze"),
         ow.node("GRU", ["x_seq", "gru.W", "gru.R", "gru.B", "", "h_in"], ["gru_Y", "h_out"], "/gru/GRU",
-                [ow.attr_int("hidden_size", H), ow.attr_int("linear_before_reset", 1)]),
+                [ow.attr_int("hidden_size", H)] + ([ow.attr_int("linear_before_reset", 1)] if lbr else [])),
         ow.node("Squeeze", ["h_out", "axes0"], ["h_t"], "/gru/Squeeze"),
     ]
     cur = "h_t"
@@ -181,6 +183,11 @@ MODELS = {
     "pipe_512_relu": lambda: mlp_model_bytes((70, 512, 512, 7), seed=12, act="Relu"),         # 8 x 1, K0 = 128
     "pipe_one_hidden": lambda: mlp_model_bytes((48, 256, 12), seed=13),                       # one hidden layer
     "gru_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=14),            # 2-tile GRU stage
+    # GRU with linear_before_reset = 0 (the attribute left at its ONNX default): the
+    # generic body's two-pass cell (fused_impl.hpp gru0_cell)
+    "gru_lbr0_small": lambda: gru_model_bytes(I=10, H=32, head=(64, 6), seed=18, lbr=0),
+    "gru_lbr0_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=19, lbr=0),
+    "go2_gru_256_lbr0": lambda: gru_model_bytes(seed=20, lbr=0),
     # LSTM policies (the other recurrent cell of exported rsl_rl / Isaac policies)
     "go2_lstm_256": lambda: lstm_model_bytes(),
     "lstm_128": lambda: lstm_model_bytes(I=30, H=128, head=(256, 256, 12), seed=15),           # 2-tile LSTM stage

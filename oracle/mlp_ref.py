@@ -56,7 +56,7 @@ ACT_DEFAULTS = {  # ONNX attribute defaults (alpha, beta) per activation
     "Sigmoid": (0.0, 0.0), "Softplus": (0.0, 0.0), "Softsign": (0.0, 0.0)}
 
 
-def mlp_layers(g: onnx_ref.Graph):
+def mlp_layers(g: onnx_ref.Graph, strict: bool = False):
     """Return [(W[N,K] f32, b[N] f32, act_name, alpha, beta)] for a Linear/act chain.
 
     Lowering rules (the ONNX semantics, restated independently of the product's
@@ -64,7 +64,11 @@ def mlp_layers(g: onnx_ref.Graph):
     min, beta = max); a constant Mul / Div right after a Gemm scales the layer's
     rows and bias; one after an activation scales the next layer's input columns
     (fp32 products in graph order). Prologue / output elementwise ops are not
-    layers (onnx_ref.act evaluates them)."""
+    layers (onnx_ref.act evaluates them); a Slice -> ... -> Concat observation
+    front-end is prologue too (the walk follows its first block to the Concat).
+    strict: raise NotImplementedError when the graph has output-side work the
+    returned layers do not carry (a Mul / Div or a Clip after the final activation),
+    so that MlpRef.from_onnx never returns a silently different policy."""
     layers = []
     cur = g.inputs[0][0]
     producers = {}
@@ -137,11 +141,15 @@ def mlp_layers(g: onnx_ref.Graph):
                 al, be = nd.attrs.get("alpha", da), nd.attrs.get("beta", db)
             layers[-1][2:5] = [op, float(np.float32(al)), float(np.float32(be))]
             last_act = True
-        elif op in ("Sub", "Div", "Mul", "Clip", "Identity", "Flatten"):
-            pass  # prologue / epilogue elementwise ops: not dense layers (onnx_ref.act evaluates them)
+        elif op in ("Sub", "Div", "Mul", "Clip", "Identity", "Flatten") or (op in ("Slice", "Concat") and not layers):
+            # prologue / epilogue elementwise ops: not dense layers (onnx_ref.act evaluates them)
+            if strict and layers and op in ("Mul", "Div", "Clip"):
+                raise NotImplementedError(f"{op} after the final activation: MlpRef would not apply it")
         else:
             raise NotImplementedError(op)
         cur = nd.outputs[0]
+    if strict and col_scale is not None:
+        raise NotImplementedError("a Mul / Div after the final activation: MlpRef would not apply it")
     return [tuple(l) for l in layers]
 
 
@@ -168,7 +176,7 @@ class MlpRef:
 
     @classmethod
     def from_onnx(cls, path):
-        return cls(mlp_layers(onnx_ref.load(path)))
+        return cls(mlp_layers(onnx_ref.load(path), strict=True))
 
     def f32(self, x, nthreads=0):
         x = np.ascontiguousarray(x, np.float32).reshape(-1, self.in_dim)

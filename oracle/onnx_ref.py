@@ -24,6 +24,10 @@ the reference's graph uses, evaluated on the reference's own weights
   linear_before_reset=1:  h~ = tanh(Wh x + Wbh + r * (Rh h + Rbh))
   linear_before_reset=0:  h~ = tanh(Wh x + Wbh + Rh (r * h) + Rbh)
   H' = (1 - z) * h~ + z * H.
+* `Slice` (opset 13; opset 1 attributes) and `Concat` (opset 13), the per-block
+  observation front-end (Slice the observation, normalise each block, Concat) an
+  exported policy may carry (numpy slicing semantics: negative indices count from
+  the end, out-of-range ones clamp, as the operator specification states).
 * `LSTM` (opset 14), the other recurrent cell exported policies use (SURVEY
   §8f.3): gate order i, o, f, c; f = sigmoid, g = h = tanh; no peepholes,
   input_forget = 0:
@@ -349,6 +353,26 @@ def _lstm(node: Node, env: dict, dt):
     return res
 
 
+def _slice(node: Node, env: dict, x):
+    """ONNX Slice: opset >= 10 takes starts / ends / axes / steps as inputs, opset 1-9
+    as attributes; negative starts / ends count from the end and out-of-range ones clamp
+    (numpy slicing does both). The loader's Slice -> ... -> Concat front-end
+    (onnx_model.cpp) is checked against this."""
+    ins = node.inputs
+    if len(ins) > 1:
+        starts, ends = (env[ins[i]].astype(np.int64).ravel() for i in (1, 2))
+        axes = env[ins[3]].astype(np.int64).ravel() if len(ins) > 3 and ins[3] else np.arange(len(starts))
+        steps = env[ins[4]].astype(np.int64).ravel() if len(ins) > 4 and ins[4] else np.ones(len(starts), np.int64)
+    else:
+        starts, ends = np.asarray(node.attrs["starts"]), np.asarray(node.attrs["ends"])
+        axes = np.asarray(node.attrs.get("axes", list(range(len(starts)))))
+        steps = np.ones(len(starts), np.int64)
+    sl = [slice(None)] * x.ndim
+    for s0, e0, ax, st in zip(starts, ends, axes, steps):
+        sl[int(ax) % x.ndim] = slice(int(s0), int(e0), int(st))
+    return x[tuple(sl)]
+
+
 def run(g: Graph, feeds: dict, dtype=np.float64) -> dict:
     """Evaluate the graph in node order with numpy in `dtype` arithmetic."""
     dt = np.dtype(dtype)
@@ -417,6 +441,10 @@ def run(g: Graph, feeds: dict, dtype=np.float64) -> dict:
             if v is None:
                 v = a.get("value_float", a.get("value_floats"))
             out = {nd.outputs[0]: np.asarray(v, dtype=dt)}
+        elif op == "Slice":
+            out = {nd.outputs[0]: _slice(nd, env, ins[0])}
+        elif op == "Concat":
+            out = {nd.outputs[0]: np.concatenate(ins, axis=int(a["axis"]))}
         elif op == "GRU":
             out = _gru(nd, env, dt)
         elif op == "LSTM":

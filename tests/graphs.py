@@ -3,7 +3,8 @@
 MatMul + Add, Sub/Div input normalisation, LeakyRelu / Sigmoid, trailing
 Tanh + Clip, Clip between dense layers (ReLU6), Constant nodes, Mul by a
 constant at the input / after a Gemm / after an activation / at the output,
-Selu / Softplus / HardSigmoid / HardSwish / Softsign. Built with the repo's own
+Selu / Softplus / HardSigmoid / HardSwish / Softsign, a Slice -> per-block
+normalisation -> Concat observation front-end. Built with the repo's own
 writer; evaluated by the oracle."""
 import numpy as np
 
@@ -128,11 +129,57 @@ def variant_bytes(kind: str, seed: int = 0) -> bytes:
                  ow.node("Selu", ["h2"], ["act"], "", [ow.attr_float("alpha", 1.2), ow.attr_float("gamma", 0.8)])]
         inits = [("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2)]
         return ow.model(nodes, inits, [("obs", ["N", 16])], [("act", ["N", 5])])
+    if kind == "slice_concat_blocks":
+        # per-block normalisation of a 2-step history (49 + 49 columns, controller.hpp:45-68):
+        # Slice each block, (x - mean) / std per block, Concat, then the shipped policy's shape
+        # (98 -> 128 -> 128 -> 12, Elu): the 4-wave pipeline and the resident kernels with a prologue
+        m0, m1 = f32(49), f32(49)
+        s0, s1 = (np.abs(f32(49)) + 0.5).astype(np.float32), (np.abs(f32(49)) + 0.5).astype(np.float32)
+        W1, b1 = (f32(128, 98) / 3).astype(np.float32), f32(128)
+        W2, b2, W3, b3 = (f32(128, 128) / 3).astype(np.float32), f32(128), (f32(12, 128) / 3).astype(np.float32), f32(12)
+        i64 = lambda *v: np.array(v, np.int64)  # noqa: E731
+        nodes = [ow.node("Slice", ["obs", "st0", "en0", "ax"], ["blk0"]),
+                 ow.node("Slice", ["obs", "st1", "en1", "ax"], ["blk1"]),
+                 ow.node("Sub", ["blk0", "m0"], ["c0"]), ow.node("Div", ["c0", "s0"], ["n0"]),
+                 ow.node("Sub", ["blk1", "m1"], ["c1"]), ow.node("Div", ["c1", "s1"], ["n1"]),
+                 ow.node("Concat", ["n0", "n1"], ["x"], "", [ow.attr_int("axis", 1)]),
+                 ow.node("Gemm", ["x", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]), ow.node("Elu", ["h1"], ["a1"]),
+                 ow.node("Gemm", ["a1", "W2", "b2"], ["h2"], "", [ow.attr_int("transB", 1)]), ow.node("Elu", ["h2"], ["a2"]),
+                 ow.node("Gemm", ["a2", "W3", "b3"], ["act"], "", [ow.attr_int("transB", 1)])]
+        inits = [("st0", i64(0)), ("en0", i64(49)), ("st1", i64(49)), ("en1", i64(2**63 - 1)), ("ax", i64(1)),
+                 ("m0", m0), ("s0", s0), ("m1", m1), ("s1", s1), ("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2),
+                 ("W3", W3), ("b3", b3)]
+        return ow.model(nodes, inits, [("obs", ["N", 98])], [("act", ["N", 12])])
+    if kind == "slice_concat_mixed":
+        # three blocks with different ops (a scalar Mul; nothing but an Identity; Sub and a
+        # per-column Mul), every block clipped to the same interval, one Slice in the opset-1
+        # attribute form and one with negative indices, then a small Tanh policy
+        k0 = np.array(1.5, np.float32)
+        sub2, mul2 = f32(10), (np.abs(f32(10)) + 0.3).astype(np.float32)
+        W1, b1, W2, b2 = f32(40, 30), f32(40), f32(6, 40), f32(6)
+        i64 = lambda *v: np.array(v, np.int64)  # noqa: E731
+        lo, hi = np.array(-1.2, np.float32), np.array(1.1, np.float32)
+        nodes = [ow.node("Slice", ["obs"], ["blk0"], "", [ow.attr_ints("starts", [0]), ow.attr_ints("ends", [7]),
+                                                        ow.attr_ints("axes", [1])]),
+                 ow.node("Slice", ["obs", "st1", "en1", "ax1"], ["blk1"]),
+                 ow.node("Slice", ["obs", "st2", "en2", "ax2", "sp2"], ["blk2"]),
+                 ow.node("Mul", ["k0", "blk0"], ["p0"]), ow.node("Clip", ["p0", "lo", "hi"], ["q0"]),
+                 ow.node("Identity", ["blk1"], ["p1"]), ow.node("Clip", ["p1", "lo", "hi"], ["q1"]),
+                 ow.node("Sub", ["blk2", "sub2"], ["c2"]), ow.node("Mul", ["c2", "mul2"], ["p2"]),
+                 ow.node("Clip", ["p2", "lo", "hi"], ["q2"]),
+                 ow.node("Concat", ["q0", "q1", "q2"], ["x"], "", [ow.attr_int("axis", -1)]),
+                 ow.node("Gemm", ["x", "W1", "b1"], ["h1"], "", [ow.attr_int("transB", 1)]), ow.node("Tanh", ["h1"], ["a1"]),
+                 ow.node("Gemm", ["a1", "W2", "b2"], ["act"], "", [ow.attr_int("transB", 1)])]
+        inits = [("st1", i64(7)), ("en1", i64(-10)), ("ax1", i64(-1)), ("st2", i64(-10)), ("en2", i64(30)),
+                 ("ax2", i64(1)), ("sp2", i64(1)), ("k0", k0), ("lo", lo), ("hi", hi), ("sub2", sub2), ("mul2", mul2),
+                 ("W1", W1), ("b1", b1), ("W2", W2), ("b2", b2)]
+        return ow.model(nodes, inits, [("obs", ["N", 30])], [("act", ["N", 6])])
     raise KeyError(kind)
 
 
 VARIANTS = ["gemm_transB0_alpha_beta", "matmul_add_sigmoid", "normalized_tanh_clip", "relu_deep", "relu6_mid_clip",
-            "relu6_pipeline", "const_scales", "selu_softplus_hardswish", "softsign_selu_attrs"]
+            "relu6_pipeline", "const_scales", "selu_softplus_hardswish", "softsign_selu_attrs", "slice_concat_blocks",
+            "slice_concat_mixed"]
 # graphs whose every operator propagates a NaN (ONNX Clip included): a NaN observation
 # row must come out as a NaN action row
 NAN_VARIANTS = ["normalized_tanh_clip", "relu6_mid_clip", "relu6_pipeline", "const_scales"]
@@ -149,7 +196,30 @@ UNSUPPORTED = {
     # Mul after the last activation, then Clip: clip(s * y) is not post_fn's clip-then-scale
     "mul_then_clip_out": lambda: _chain([], tail=[("Tanh",), ("Mul", np.float32(2.0)), ("Clip", -1.0, 1.0)]),
     "vector_mul_out": lambda: _chain([], tail=[("Tanh",), ("Mul", np.arange(1, 5, dtype=np.float32))]),
+    # observation front-ends the per-column prologue cannot express: blocks Concatenated out
+    # of order (a column permutation), and blocks clipped to different intervals
+    "slice_reordered": lambda: _front([(4, 8), (0, 4)], clips=None),
+    "slice_clip_differs": lambda: _front([(0, 4), (4, 8)], clips=[(-1.0, 1.0), (-2.0, 2.0)]),
 }
+
+
+def _front(blocks, clips):
+    """obs[8] -> Slice blocks (-> Clip) -> Concat -> Gemm -> act[3] (refusal cases)."""
+    r = _rng(6)
+    inits = [("W", r.standard_normal((3, 8)).astype(np.float32)), ("ax", np.array([1], np.int64))]
+    nodes, outs = [], []
+    for i, (b, e) in enumerate(blocks):
+        inits += [(f"s{i}", np.array([b], np.int64)), (f"e{i}", np.array([e], np.int64))]
+        nodes.append(ow.node("Slice", ["obs", f"s{i}", f"e{i}", "ax"], [f"b{i}"]))
+        out = f"b{i}"
+        if clips:
+            inits += [(f"lo{i}", np.array(clips[i][0], np.float32)), (f"hi{i}", np.array(clips[i][1], np.float32))]
+            nodes.append(ow.node("Clip", [out, f"lo{i}", f"hi{i}"], [f"c{i}"]))
+            out = f"c{i}"
+        outs.append(out)
+    nodes += [ow.node("Concat", outs, ["x"], "", [ow.attr_int("axis", 1)]),
+              ow.node("Gemm", ["x", "W"], ["act"], "", [ow.attr_int("transB", 1)])]
+    return ow.model(nodes, inits, [("obs", [1, 8])], [("act", [1, 3])])
 
 
 def _chain(mid_ops, tail=()):

@@ -84,7 +84,7 @@ def test_loader_synthetic(synth_path, name):
     _check_layers(engine.inspect_model(p), _oracle_layers(p))
 
 
-@pytest.mark.parametrize("name", ["gru_small", "go2_gru_256"])
+@pytest.mark.parametrize("name", ["gru_small", "go2_gru_256", "gru_lbr0_small"])
 def test_loader_gru(synth_path, name):
     from go2_onnx_controller_amd import engine
     from oracle import onnx_ref
@@ -93,7 +93,8 @@ def test_loader_gru(synth_path, name):
     g = onnx_ref.load(p)
     gru = next(n for n in g.nodes if n.op_type == "GRU")
     W, R, B = (g.inits[gru.inputs[i]].astype(np.float64) for i in (1, 2, 3))
-    assert v["gru"]["H"] == R.shape[2] and v["gru"]["I"] == W.shape[2] and v["gru"]["lbr"] == 1
+    assert v["gru"]["H"] == R.shape[2] and v["gru"]["I"] == W.shape[2]
+    assert v["gru"]["lbr"] == (0 if "lbr0" in name else 1)
     assert v["gru"]["w_sum"] == pytest.approx(W.sum(), rel=1e-9)
     assert v["gru"]["r_sum"] == pytest.approx(R.sum(), rel=1e-9)
     assert v["gru"]["b_sum"] == pytest.approx(B.sum(), rel=1e-9)
@@ -117,13 +118,20 @@ def test_loader_graph_variants(tmp_path, kind):
     if kind == "const_scales":
         assert v["pre_mul"] == 20 and v["pre_clip"] == pytest.approx([-2.5, 2.0])
         assert v["clip"] == pytest.approx([-0.4, 0.9]) and v["post_scale"] == 0.25
+    if kind == "slice_concat_blocks":  # two blocks' (x - mean) / std: one per-column prologue
+        assert (v["in_dim"], v["pre_sub"], v["pre_div"], v["pre_mul"]) == (98, 98, 98, 0)
+    if kind == "slice_concat_mixed":  # a scalar Mul, an Identity, Sub + Mul; one shared Clip
+        assert (v["pre_sub"], v["pre_div"], v["pre_mul"]) == (30, 0, 30)
+        assert v["pre_clip"] == pytest.approx([-1.2, 1.1])
 
 
 @pytest.mark.parametrize("kind,msg", [("conv", "unsupported operator 'Conv'"),
                                       ("dynamic_weight", "not an initializer"),
                                       ("clip_after_act_mid", "only supported at the end of the graph"),
                                       ("mul_then_clip_out", "Clip after a Mul"),
-                                      ("vector_mul_out", "per-feature Mul after the final activation")])
+                                      ("vector_mul_out", "per-feature Mul after the final activation"),
+                                      ("slice_reordered", "cover its columns in order"),
+                                      ("slice_clip_differs", "Clip bounds differ")])
 def test_loader_rejects_unsupported(tmp_path, kind, msg):
     from go2_onnx_controller_amd import engine
     with pytest.raises(engine.Go2piError, match=msg):

@@ -59,6 +59,55 @@ def test_gru256_batch_4096_ticks(synth_path, waves):
         assert abs_err(e.get_hidden(B), want_h) <= TOL
 
 
+# linear_before_reset = 0 (n = tanh(Wh x + Wbh + Rh (r . h) + Rbh)): the generic body's
+# two-pass cell on every path the graph-variant tests cover — batch 1 and 5 with a launch
+# per call or the resident option (which serves lbr = 0 by a launch too), and batch 300
+@pytest.mark.parametrize("name", ["gru_lbr0_small", "gru_lbr0_128", "go2_gru_256_lbr0"])
+@pytest.mark.parametrize("B,res", [(1, 0), (1, 100), (5, 0), (5, 100), (300, 0)])
+def test_gru_lbr0_rollout(synth_path, name, B, res):
+    from go2_onnx_controller_amd import Engine
+    p = synth_path(name)
+    with Engine(p, max_batch=512, resident_ms=res) as e:
+        rng = np.random.default_rng(B + res)
+        T = 5
+        xs = rng.standard_normal((T, B, e.in_dim)).astype(np.float32)
+        want_y, want_h = _oracle_rollout(p, xs)
+        e.reset_hidden()
+        for t in range(T):
+            assert abs_err(e.run(xs[t]), want_y[t]) <= TOL, t
+        assert abs_err(e.get_hidden(B), want_h) <= TOL
+
+
+def test_gru_lbr0_differs_from_lbr1(synth_path):
+    """The two GRU forms are different functions of the same weights: the oracle's lbr=0
+    rollout is not the lbr=1 one (so the test above pins the lbr=0 cell itself)."""
+    from oracle import onnx_ref
+    g = onnx_ref.load(synth_path("gru_lbr0_small"))
+    x = np.random.default_rng(3).standard_normal((2, 4, 10))
+    y0, _ = _oracle_rollout(synth_path("gru_lbr0_small"), x)
+    cell = next(n for n in g.nodes if n.op_type == "GRU")
+    cell.attrs["linear_before_reset"] = 1
+    h = np.zeros((1, 4, 32))
+    y1 = onnx_ref.run(g, {"observation": x[0], "h_in": h})["action"]
+    assert np.abs(y1 - y0[0]).max() > 1e-4
+
+
+def test_gru_lbr0_sequence_matches_ticks(synth_path):
+    """run_sequence (h in LDS across ticks) with the two-pass lbr = 0 cell."""
+    import torch
+    from go2_onnx_controller_amd import Engine
+    p = synth_path("gru_lbr0_128")
+    T, B = 6, 300
+    x = torch.randn(T, B, 30, device="cuda:0")
+    with Engine(p, max_batch=B) as a:
+        ya = a.run_sequence_torch(x)
+        torch.cuda.synchronize()
+        ha = a.get_hidden(B)
+    want_y, want_h = _oracle_rollout(p, x.cpu().numpy())
+    assert abs_err(ya.cpu().numpy(), want_y) <= TOL
+    assert abs_err(ha, want_h) <= TOL
+
+
 def test_gru_sequence_lds_carry_matches_ticks(synth_path):
     """run_sequence keeps h in LDS across ticks; identical math to per-tick calls."""
     import torch
