@@ -224,8 +224,9 @@ def gru_leg(device, launches=20, seq_ticks=100):
         out["kernel"] = e.batched_kernel
         out["robots"] = B
         # memory-side bytes of one 100-tick launch (committed rocprofv3 FETCH/WRITE passes)
-        tr = load_pmc("go2_gru_256_b4096_seq100", e.batched_kernel)
+        tr, note = load_pmc("go2_gru_256_b4096_seq100", e.batched_kernel)
         out["seq100"]["traffic_bytes_per_launch"] = round(tr) if tr else None
+        out["seq100"]["traffic_source"] = note
     return out
 
 
@@ -311,21 +312,29 @@ def controller_leg(device, steps=200, warm=20, iters=10000):
 
 
 def load_pmc(workload, kernel):
-    """Memory-side bytes per launch of the batched kernel instantiation `kernel`
-    (e.g. "policy_mlp_kernel<8, 1, 3, 1, 3>", Engine.batched_kernel) from the
-    committed rocprofv3 --pmc summary of this workload (tools/profile.sh +
-    tools/summarize_prof.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read
-    correction x2). None when no summary of this exact kernel is committed."""
+    """(bytes, note): memory-side bytes per launch of the batched kernel
+    instantiation `kernel` (e.g. "policy_mlp_kernel<8, 1, 3, 1, 3>",
+    Engine.batched_kernel) from the committed rocprofv3 --pmc summary of this
+    workload (tools/profile.sh + tools/summarize_prof.py: separate FETCH_SIZE /
+    WRITE_SIZE passes, gfx950 read correction x2), and where it came from. bytes is
+    None, with the reason in note, when no summary of this exact kernel is committed
+    or the kernel sources changed after it was taken (provenance.kernel_source_digest)."""
+    from go2_onnx_controller_amd.provenance import kernel_source_digest
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
         for k, v in d.get("workloads", {}).get(workload, {}).items():
             if f"::{kernel}(" in k:
-                return v.get("hbm_bytes_per_launch")
+                src = v.get("source", "?")
+                if v.get("src_digest") != kernel_source_digest():
+                    return None, (f"stale: profiles/{src} was taken on other kernel sources "
+                                  f"(digest {v.get('src_digest')}, now {kernel_source_digest()}); re-profile")
+                return v.get("hbm_bytes_per_launch"), f"profiles/{src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
     except (OSError, ValueError):
         pass
-    return None
+    return None, "no committed rocprofv3 --pmc summary of this kernel"
+
 
 
 def _free_port():
@@ -508,7 +517,7 @@ def main():
         bytes_launch = cost["weight_bytes"] + cost["io_bytes_per_row"] * batch * ticks
         achieved_tf = flops_launch / (kernel_ms * 1e-3) / 1e12
         kernel_name = eng.batched_kernel
-        traffic = load_pmc(args.workload, kernel_name)
+        traffic, traffic_note = load_pmc(args.workload, kernel_name)
         eng.close()
         out.update({
             "kernel": kernel_name,
@@ -519,6 +528,7 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4),
                          "frac_per_gpu_min": round(flops_launch / (k_max * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic,
+                         "traffic_source": traffic_note,
                          "algorithmic_flops_per_launch": flops_launch,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "hbm_frac": round(bytes_launch / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)},

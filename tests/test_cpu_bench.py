@@ -47,3 +47,26 @@ def test_bench_failing_rank_fails_the_job():
     # must fail the job with a non-zero status, not leave the launcher waiting
     r = _run(["--gpus", "2", "--dry-run", "--steps", "1", "--dist-backend", "nccl"], timeout=120)
     assert r.returncode != 0
+
+
+def test_traffic_null_when_profile_is_stale(tmp_path, monkeypatch):
+    """roofline.traffic comes from the committed --pmc summary only while the kernel
+    sources are the ones it was measured on: a summary entry
+    with another source digest yields None and says why."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from go2_onnx_controller_amd.provenance import kernel_source_digest
+    kern = "policy_mlp_kernel<8, 1, 3, 1, 3>"
+    name = f"void go2pi::{kern}(go2pi::DevProgram const*, float const*, float*, int)"
+    (tmp_path / "profiles").mkdir()
+    summary = tmp_path / "profiles" / "pmc_summary.json"
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    for digest, want in [(kernel_source_digest(), 19.0e6), ("0123456789abcdef", None), (None, None)]:
+        entry = {"hbm_bytes_per_launch": 19.0e6, "source": "rXX_mlp512_kernel_stats.csv"}
+        if digest:
+            entry["src_digest"] = digest
+        summary.write_text(json.dumps({"workloads": {"go2_mlp_512_b4096": {name: entry}}}))
+        got, note = bench.load_pmc("go2_mlp_512_b4096", kern)
+        assert got == want, note
+        assert ("stale" in note) == (want is None)
+    assert bench.load_pmc("other_workload", kern) == (None, "no committed rocprofv3 --pmc summary of this kernel")

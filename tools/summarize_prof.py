@@ -59,6 +59,10 @@ def main():
     except (OSError, ValueError):
         summary = {}
     summary.pop("kernels", None)
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2_onnx_controller_amd.provenance import kernel_source_digest
+    digest = kernel_source_digest()  # the sources the profiled library was built from (bench.py checks it)
     wl = summary.setdefault("workloads", {}).setdefault(args.workload, {})
     for name in dur:
         if name.startswith("__amd"):
@@ -69,7 +73,7 @@ def main():
         wl[name] = {"avg_ns": dur[name], "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                                     "hbm_bytes_per_launch": hbm, "source": os.path.basename(stats_dst),
                                     "correction": "read bytes = 2 x FETCH_SIZE (gfx950, 16-B/lane streams)",
-                                    "note": args.note}
+                                    "note": args.note, "src_digest": digest}
     with open(os.path.join(prof, f"{args.round}_{args.tag}_pmc.csv"), "w", newline="") as fh:
         w = csv.writer(fh)
         w.writerow(["kernel", "calls", "avg_ns", "FETCH_SIZE_KiB", "WRITE_SIZE_KiB", "traffic_bytes_corrected"])
