@@ -394,6 +394,18 @@ struct go2pi_engine {
       // (h_err set) is a device-side protocol fault and is reported, not retried
       need_device();
       resident_stop();
+      if (!ctl) {  // the kernel has exited (stream synced): a request it served has every granule
+        const int nout = (int)batch * model.out_dim;
+        int k = 0;
+        while (k < nout && (unsigned)(__atomic_load_n(h_actg + k, __ATOMIC_ACQUIRE) >> 32) == e0) ++k;
+        if (k == nout) {
+          for (int j = 0; j < nout; ++j) {
+            const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
+            std::memcpy(h_act + j, &bits, 4);
+          }
+          return true;
+        }
+      }
       if (__atomic_load_n(h_err, __ATOMIC_ACQUIRE)) {
         __atomic_store_n(h_err, 0u, __ATOMIC_RELEASE);
         throw HipError("resident kernel: a layer hand-off timed out (request not served)", GO2PI_E_DEVICE);

@@ -865,8 +865,15 @@ Model parse_onnx(const uint8_t *data, size_t n) {
       v = std::move(r);
     };
     const bool lstm = m.gru.cell == 1;
-    reorder(m.inputs, trace_in(5), lstm ? trace_in(6) : -1);
-    reorder(m.outputs, trace_out(1), lstm ? trace_out(2) : -1);
+    const long hi = trace_in(5), ci = lstm ? trace_in(6) : -1, ho = trace_out(1), co = lstm ? trace_out(2) : -1;
+    //  the state I/O is (h) or (h, c) positionally after the observation /
+    // action (actor.py maps them so): an LSTM exposes both or neither, and h and c are
+    // distinct graph values
+    if (lstm && ((hi >= 0) != (ci >= 0) || (ho >= 0) != (co >= 0)))
+      fail("LSTM: initial_h / initial_c (and Y_h / Y_c) must both be graph I/O, or neither");
+    if ((hi >= 0 && hi == ci) || (ho >= 0 && ho == co)) fail(std::string(lstm ? "LSTM" : "GRU") + ": h and c trace to the same graph I/O");
+    reorder(m.inputs, hi, ci);
+    reorder(m.outputs, ho, co);
   }
   if (!col_scale.empty()) {
     if (col_scale.size() != 1) fail("a per-feature Mul after the final activation is unsupported");

@@ -741,10 +741,12 @@ __global__ __launch_bounds__(RES_WAVES * 64) void policy_resident_kernel(const D
   }
   if (g == 0 && tid == 0)
     __hip_atomic_store(mirror, (u64)GO2PI_RES_LEAVE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (g == 0 && tid == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  // every wave's stores (wave RES_PW's answer granules among them) drained before the
+  // LEAVE done word: a host that sees LEAVE and rescans finds a served request's answer
+  // (engine.cpp resident_serve)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (g == 0 && tid == 0) __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -842,7 +844,9 @@ unsigned r1_lgs(const DevProgram &p, int nt) {
 
 bool resident1_fits(const DevProgram &p, bool ctl) {
   const int nt = ctl ? 512 : 1024;
-  if (p.has_gru || p.nl < 1 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
+  // (nl >= 2: with one layer nothing would separate the request loop's top barrier from
+  // the polling wave's next writes of st / x0)
+  if (p.has_gru || p.nl < 2 || p.nl > R1_LMAX || p.L[p.nl - 1].N_pad != 16) return false;
   for (int l = 0; l < p.nl; ++l) {
     const int thr = l == p.nl - 1 ? nt - 64 : nt;
     const int G = r1_group(p.L[l].N_pad, thr);
@@ -1079,10 +1083,11 @@ __global__ __launch_bounds__(NT) void policy_resident1_kernel(const DevProgram *
     }
     ++nreq;
   }
-  if (tid == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  // every wave's answer stores drained before the LEAVE done word (the final layer's
+  // granules come from waves 1..15)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1111,43 +1116,70 @@ __global__ __launch_bounds__(NT) void policy_resident1_kernel(const DevProgram *
 // Summation order per output: two packed fma chains per register (x.xy, x.zw)
 // over the lane's float4s, their sum, then the fixed DPP tree: deterministic,
 // within the 1e-5 contract of the fp64 oracle (not the MFMA path's order).
-constexpr int A1_CW = 8;                 // compute waves
-constexpr int A1_NT = 64 * (1 + A1_CW);  // + the polling wave
-constexpr int A1_NP = 2;                 // granule loads per lane per sweep (header + <= 127 obs floats)
+constexpr int A1_NP = 2;  // granule loads per lane per sweep (header + <= 127 obs floats)
+// threads of the form with CW compute waves (+ the polling wave)
+__host__ __device__ constexpr int a1_nt(int cw) { return 64 * (1 + cw); }
 
-// the weight register of output r ... : lane s of a row keeps output
-// r(j, s) = j ^ 2 [s >= 8] ^ [(s >> 2) & 1] in register j (R = 4), j ^ [s >= 8] (R = 2),
-// so that every step of the reduce-scatter adds the same register index of its partner
+// The weight register of each output: lane s of a row keeps output r(j, s) in register
+// j, so that every step of the reduce-scatter adds the same register index of its
+// partner (s ^ 8, then s ^ 7, s ^ 2, s ^ 1):
+//   R = 8: r = j ^ 4 b3 ^ 3 b2 ^ b1,  R = 4: r = j ^ 2 b3 ^ b2,  R = 2: r = j ^ b3
+// (b_i: bit i of s). After the reduce-scatter lane s holds output a1_out(0, s).
 template <int R>
 __device__ __forceinline__ int a1_out(int j, int s) {
-  if constexpr (R == 4) return j ^ ((s >> 3) << 1) ^ ((s >> 2) & 1);
+  if constexpr (R == 8) return j ^ ((s >> 3) << 2) ^ (3 * ((s >> 2) & 1)) ^ ((s >> 1) & 1);
+  else if constexpr (R == 4) return j ^ ((s >> 3) << 1) ^ ((s >> 2) & 1);
   else if constexpr (R == 2) return j ^ (s >> 3);
   else return 0;
 }
-// after the reduce-scatter lane s holds the row's output a1_fin(s) (R = 4: its quad)
 template <int R>
 __device__ __forceinline__ int a1_fin(int s) {
-  if constexpr (R == 4) return s >> 2;
-  else if constexpr (R == 2) return s >> 3;
-  else return 0;
+  return a1_out<R>(0, s);
+}
+
+// a + dpp(b) in one v_add_f32_dpp (the compiler kept each v_mov_b32_dpp apart from
+// its add, and with two waves per SIMD every instruction of the chain costs issue
+// slots); the s_nop covers the VALU-write -> DPP-read hazard (2 wait states)
+template <int CTRL>
+__device__ __forceinline__ float a1_dadd(float a, float b) {
+  float r;
+  if constexpr (CTRL == 0x128)
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 row_ror:8 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a));
+  else if constexpr (CTRL == 0x141)
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 row_half_mirror row_mask:0xf bank_mask:0xf"
+                 : "=v"(r) : "v"(b), "v"(a));
+  else if constexpr (CTRL == 0x4E)
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=v"(r) : "v"(b), "v"(a));
+  else
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+                 : "=v"(r) : "v"(b), "v"(a));
+  return r;
 }
 
 template <int R>
 __device__ __forceinline__ float a1_reduce(float (&p)[R]) {
-  if constexpr (R == 4) {
-    p[0] += dpp_f<0x128>(p[2]);  // row_ror:8 (lane s ^ 8): the partner keeps the other pair
-    p[1] += dpp_f<0x128>(p[3]);
-    p[0] += dpp_f<0x141>(p[1]);  // row_half_mirror (s ^ 7 within 8)
+  if constexpr (R == 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = a1_dadd<0x128>(p[j], p[j + 4]);  // row_ror:8 (lane s ^ 8)
+    p[0] = a1_dadd<0x141>(p[0], p[2]);                                  // row_half_mirror (s ^ 7 within 8)
+    p[1] = a1_dadd<0x141>(p[1], p[3]);
+    p[0] = a1_dadd<0x4E>(p[0], p[1]);  // quad_perm [2, 3, 0, 1] (s ^ 2)
+  } else if constexpr (R == 4) {
+    p[0] = a1_dadd<0x128>(p[0], p[2]);
+    p[1] = a1_dadd<0x128>(p[1], p[3]);
+    p[0] = a1_dadd<0x141>(p[0], p[1]);
+    p[0] = a1_dadd<0x4E>(p[0], p[0]);
   } else if constexpr (R == 2) {
-    p[0] += dpp_f<0x128>(p[1]);
-    p[0] += dpp_f<0x141>(p[0]);
+    p[0] = a1_dadd<0x128>(p[0], p[1]);
+    p[0] = a1_dadd<0x141>(p[0], p[0]);
+    p[0] = a1_dadd<0x4E>(p[0], p[0]);
   } else {
-    p[0] += dpp_f<0x128>(p[0]);
-    p[0] += dpp_f<0x141>(p[0]);
+    p[0] = a1_dadd<0x128>(p[0], p[0]);
+    p[0] = a1_dadd<0x141>(p[0], p[0]);
+    p[0] = a1_dadd<0x4E>(p[0], p[0]);
   }
-  p[0] += dpp_f<0x4E>(p[0]);  // quad_perm [2, 3, 0, 1]
-  p[0] += dpp_f<0xB1>(p[0]);  // quad_perm [1, 0, 3, 2]
-  return p[0];
+  return a1_dadd<0xB1>(p[0], p[0]);  // quad_perm [1, 0, 3, 2] (s ^ 1)
 }
 
 // One sweep's granule i of the request (i = u * 64 + lane; 0 = header) into layer 0's
@@ -1273,13 +1305,17 @@ __device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned
 // 16-output head. F0: layer 0's float4s per lane (K0_pad <= 64 F0). AS: the layers'
 // activation kinds, 4 bits each (layer l at 4l; the shipped model: 0x0111), or
 // 0xFFFFFFFF: read at run time. D: poll sweeps in flight. PRO: the program has an
-// observation prologue (Sub / Div / Mul / Clip), applied by the polling wave.
-template <int NL, int H, int F0, unsigned AS, int D, bool PRO>
-__global__ __launch_bounds__(A1_NT) void policy_act1_kernel(const DevProgram *__restrict__ Pd, const u64 *req,
-                                                            u64 *actg, unsigned *err, unsigned *done,
-                                                            u64 idle_ticks, const unsigned *yield) {
-  static_assert(NL >= 2 && NL <= 4 && (H == 64 || H == 128) && F0 >= 1 && F0 <= 4, "policy_act1_kernel shape");
-  constexpr int R = H / 32;   // outputs per lane in a wide layer
+// observation prologue (Sub / Div / Mul / Clip), applied by the polling wave. CW:
+// compute waves, 8 (two per SIMD, R = H / 32 outputs per lane) or 4 (one per SIMD,
+// R = H / 16: twice the weights per lane, half the lanes' reduction overhead).
+template <int NL, int H, int F0, unsigned AS, int D, bool PRO, int CW = 8>
+__global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram *__restrict__ Pd, const u64 *req,
+                                                                u64 *actg, unsigned *err, unsigned *done,
+                                                                u64 idle_ticks, const unsigned *yield) {
+  static_assert(NL >= 2 && NL <= 4 && (H == 64 || H == 128) && F0 >= 1 && F0 <= 4 && (CW == 4 || CW == 8),
+                "policy_act1_kernel shape");
+  constexpr int NT = a1_nt(CW);
+  constexpr int R = H / (4 * CW);  // outputs per lane in a wide layer (a DPP row of 16 lanes: 16 R / 16)
   constexpr int HF = H / 64;  // float4s per lane of a K = H layer
   constexpr int NM = NL - 2 > 0 ? NL - 2 : 1;  // wide layers after layer 0 (array extent)
   const DevProgram &P = *Pd;
@@ -1354,7 +1390,7 @@ __global__ __launch_bounds__(A1_NT) void policy_act1_kernel(const DevProgram *__
     const int i = u * 64 + lane;
     pk[u] = (PRO && wave == 0 && i >= 1) ? pro_k(pro, (i - 1) % in_dim) : ProK{0.f, 1.f, 1.f};
   }
-  for (int i = tid; i < GO2PI_SMALL_MAXB * S; i += A1_NT) x0[i] = 0.f;
+  for (int i = tid; i < GO2PI_SMALL_MAXB * S; i += NT) x0[i] = 0.f;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): weights and constants in registers before the first wait
   const unsigned y0 = __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // x0 cleared before the poller writes a row into it
@@ -1540,23 +1576,29 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
   const A1Shape a1 = act1_shape(p);
   if (a1.nl && !std::getenv("GO2PI_RES_R1W")) {
     const size_t lds1 = sizeof(float) * (3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4);
-    auto go1 = [&](auto kern) {
+    auto go1 = [&](auto kern, int cw) {
       if (lds1 > 64 * 1024) {
         const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
         if (a != hipSuccess) return (int)a;
       }
       // (yield never null: the kernel loads it unconditionally, see a1_poll)
-      hipLaunchKernelGGL(kern, dim3(1), dim3(A1_NT), lds1, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
+      hipLaunchKernelGGL(kern, dim3(1), dim3(a1_nt(cw)), lds1, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
                          err, done, idle_ticks, yield ? yield : reinterpret_cast<const unsigned *>(p.zero));
       return (int)hipGetLastError();
     };
     const char *dv = std::getenv("GO2PI_A1_DEPTH");
     const int depth = dv ? std::atoi(dv) : 2;
     const bool pro = p.pre_sub || p.pre_div || p.pre_mul || p.pre_clip;
+    const char *cv = std::getenv("GO2PI_A1_CW");
+    const int cw = cv && std::atoi(cv) == 4 ? 4 : 8;
     if (a1.nl == 4 && a1.h == 128 && a1.f0 == 2 && elu1 && !pro) {
-      if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false>);
-      return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 2, false>);
+      if (cw == 8) {
+        if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false, 8>, 8);
+        return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 2, false, 8>, 8);
+      }
+      if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false, 4>, 4);
+      return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 2, false, 4>, 4);
     }
   }
   if (p.nl == 4 && elu1 && r1_shape(p, 1024) == 0x2444u && r1_lgs(p, 1024) == 0x4333u)

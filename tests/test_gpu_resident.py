@@ -27,11 +27,13 @@ def _models(synth_path):
 
 # resident forms: "one" the single-workgroup kernel (the default where the weights fit
 # one CU: the shipped model; r05 policy_act1_kernel, a polling wave + 8 compute waves,
-# two poll sweeps in flight), "one_d1" the same with one sweep in flight, "one_r1w" the
+# two poll sweeps in flight), "one_d1" the same with one sweep in flight, "one_c4" with
+# four compute waves instead of eight, "one_r1w" the
 # r04 1024-thread form (GO2PI_RES_R1W=1), "multi" the multi-workgroup kernel
 # (GO2PI_RES_MULTI=1 for the shipped model; the only form for mlp512), "tiled0" multi
 # with layer 0 tiled like every other layer (bit-identical to the launch path)
-@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "one_d1"), ("shipped", "one_r1w"),
+@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "one_d1"), ("shipped", "one_c4"),
+                                       ("shipped", "one_r1w"),
                                        ("shipped", "multi"), ("shipped", "tiled0"),
                                        ("mlp512", "multi"), ("mlp512", "tiled0")])
 def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
@@ -40,6 +42,8 @@ def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
     tiled0 = form == "tiled0"
     if form == "one_d1":
         monkeypatch.setenv("GO2PI_A1_DEPTH", "1")  # read at each resident launch
+    elif form == "one_c4":
+        monkeypatch.setenv("GO2PI_A1_CW", "4")  # four compute waves (one per SIMD)
     elif form == "one_r1w":
         monkeypatch.setenv("GO2PI_RES_R1W", "1")
     elif form != "one":
@@ -420,6 +424,60 @@ def test_batched_launch_evicts_other_resident_kernels(synth_path):
             th.join(timeout=10)
     assert not errs, errs
     assert n_act[0] > 10
+
+
+def test_small_batched_launch_beside_busy_resident_kernel(synth_path):
+    """A batched launch of <= GO2PI_YIELD_MIN_GRID workgroups (1024 rows) evicts no
+    resident kernel: it fits on the CUs the resident kernels leave free.
+    While another engine's resident kernel answers act() at ~1 kHz from another thread,
+    1024-row launches of the 48->512^3->12 policy stay correct and bounded: their median
+    wall time stays within 3x the same launch with no resident kernel live."""
+    import threading
+    import torch
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    pb = synth_path("go2_mlp_512")
+    ra, rb = mlp_ref.MlpRef.from_onnx(SHIPPED), mlp_ref.MlpRef.from_onnx(pb)
+    xb = torch.randn((1024, 48), device="cuda:0")
+    s = torch.cuda.Stream()
+
+    def timed(b, n=40):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            yb = b.run_torch(xb, stream=s)
+            s.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[n // 2], yb
+    errs, n_act = [], [0]
+    stop = threading.Event()
+    with Engine(pb, max_batch=4096) as b:
+        alone, _ = timed(b)
+        with Engine(SHIPPED, max_batch=8, resident_ms=1000) as a:
+            x1 = realistic_obs(1, seed=4)
+            want1 = ra.f64(x1)
+            a.run(x1)  # the resident kernel is live before the launches start
+
+            def tick():
+                try:
+                    while not stop.is_set():
+                        if abs_err(a.run(x1), want1) > TOL:
+                            errs.append("act() output changed")
+                        n_act[0] += 1
+                        time.sleep(0.001)
+                except Exception as ex:  # noqa: BLE001 - reported below
+                    errs.append(repr(ex))
+            th = threading.Thread(target=tick)
+            th.start()
+            try:
+                busy, yb = timed(b)
+            finally:
+                stop.set()
+                th.join(timeout=10)
+    assert not errs, errs
+    assert n_act[0] > 10
+    assert abs_err(yb.cpu().numpy(), rb.f64(xb.cpu().numpy())) <= TOL
+    assert busy <= 3 * alone + 2e-4, (busy, alone)
 
 
 @pytest.mark.parametrize("name", ["gru_128", "lstm_128"])

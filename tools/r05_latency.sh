@@ -1,9 +1,9 @@
 #!/bin/bash
 # r05 batch-1 latency A/B on the GPU box: the drop-in ONNXActor::act() timed from C++
 # (as the reference's main.cpp:38-42 times it) for the shipped model, alternating the
-# r05 one-workgroup kernel (policy_act1_kernel: polling wave + 8 compute waves, two poll
-# sweeps in flight; default), the same with one sweep (GO2PI_A1_DEPTH=1), the r04
-# 1024-thread form (GO2PI_RES_R1W=1) and a launch per call (GO2PI_RESIDENT_MS=0);
+# r05 one-workgroup kernel (policy_act1_kernel: polling wave + 4 or 8 compute waves,
+# GO2PI_A1_CW; one or two poll sweeps in flight, GO2PI_A1_DEPTH), the r04 1024-thread form
+# (GO2PI_RES_R1W=1) and a launch per call (GO2PI_RESIDENT_MS=0);
 # then, with a resclk build present, the request timeline (tools/res_timeline.py).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -13,10 +13,12 @@ L=$R/go2_onnx_controller_amd/lib
 g++ -std=c++20 -O2 -I$R/include $R/tests/cpp/controller_shape.cpp -L$L -lonnx_actor -Wl,-rpath,$L -o $R/build/controller_shape || exit 1
 M=$R/tests/golden/model.onnx
 for round in 1 2 3; do
-  for v in a1d2 a1d1 r1w launch; do
+  for v in ${VARIANTS:-c4d2 c4d1 c8d2 c8d1 r1w launch}; do
     case $v in
-      a1d2) env="" ;;
-      a1d1) env="GO2PI_A1_DEPTH=1" ;;
+      c4d2) env="GO2PI_A1_CW=4" ;;
+      c4d1) env="GO2PI_A1_CW=4 GO2PI_A1_DEPTH=1" ;;
+      c8d2) env="GO2PI_A1_CW=8" ;;
+      c8d1) env="GO2PI_A1_CW=8 GO2PI_A1_DEPTH=1" ;;
       r1w) env="GO2PI_RES_R1W=1" ;;
       launch) env="GO2PI_RESIDENT_MS=0" ;;
     esac
