@@ -174,10 +174,13 @@ __device__ __forceinline__ float ctl_pro(const CtlQ &q, float x, int k) {
 // its prologue value to dst[r * ds + k]. NaN among the appended values of blocks
 // 0-5 — where the reference's populate_buffer check exit(1)s
 // (controller.hpp:57-64) — sets nanf[r] (a relaxed workgroup-scope LDS or: no fence).
+// nanm: bit r set when a value of row r is NaN (OR-ed into L.nanf once per thread by
+// ctl_nan_flush: a workgroup-scope LDS atomic per element, on the few addresses of 16
+// rows, serialised in the LDS pipeline).
 template <int BK, bool TILE, bool ARITH>
 __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, bool joy, int nrows,
                                                  float *__restrict__ dst, int ds, float *__restrict__ raw, int tid,
-                                                 int nt) {
+                                                 int nt, unsigned &nanm) {
   const float *__restrict__ obs_l = L.obs;
   const float *__restrict__ st_l = L.st;
   const float *__restrict__ jy_l = L.jy;
@@ -217,23 +220,42 @@ __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, 
     } else {  // contacts: foot_force >= 22 with the FL/FR, RL/RR swap (controller.hpp:99-103)
       x = st[31 + (c ^ 1)] >= q.thr ? 1.f : 0.f;
     }
-    if constexpr (BK < 6)
-      __hip_atomic_fetch_or(L.nanf + r, __builtin_isnan(x) ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (BK < 6) nanm |= (__builtin_isnan(x) ? 1u : 0u) << r;
     if constexpr (TILE) raw[r * in_dim + k] = x;
     dst[r * ds + k] = ctl_pro<TILE, ARITH>(q, x, k);
   }
 }
 
+__device__ __forceinline__ void ctl_nan_flush(const CtlLds L, unsigned nanm) {
+  while (nanm) {  // (a NaN observation: rare)
+    const int r = __builtin_ctz(nanm);
+    nanm &= nanm - 1;
+    __hip_atomic_fetch_or(L.nanf + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// The appended blocks that read no previous observation row (all but vel_cmd, block 2,
+// which keeps the previous command without a joystick): they can run while the
+// previous rows are still in flight (ctl_assemble_split).
+template <bool TILE, bool ARITH>
+__device__ __forceinline__ void ctl_append_noobs(const CtlLds L, const CtlQ &q, bool joy, int nrows,
+                                                 float *__restrict__ dst, int ds, float *__restrict__ raw, int tid,
+                                                 int nt, unsigned &nanm) {
+  ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<4, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<5, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<6, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+}
+
 template <bool TILE, bool ARITH>
 __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ &q, bool joy, int nrows, float *__restrict__ dst,
                                            int ds, float *__restrict__ raw, int tid, int nt) {
-  ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<2, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<4, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<5, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
-  ctl_append_block<6, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt);
+  unsigned nanm = 0u;
+  ctl_append_noobs<TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<2, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_nan_flush(L, nanm);
 }
 
 // The shifted values (std::shift_left by d, controller.hpp:45-52): column k of
@@ -299,7 +321,7 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nro
 template <bool TILE, int UNR = 4>
 __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt) {
-  // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
+    // (GO2PI_DIAG_CLOCK: thread 0's time after each pass, slots 50-51)
   if (TILE && (q.pro.sub || q.pro.div || q.pro.mul)) {
     ctl_append<TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt);
     GO2PI_STAMP(P, tid == 0, 50);
@@ -316,6 +338,51 @@ __device__ __forceinline__ void ctl_assemble_flat(const DevProgram &P, const Ctl
   ctl_shift<TILE, false, UNR>(L, q, nrows, dst, ds, raw, tid, nt);
   GO2PI_STAMP(P, tid == 0, 53);
 #endif
+}
+
+// ctl_assemble_flat in two parts around `mid` (the caller's wait for the previous
+// observation rows and a barrier): the blocks that read only the state, joystick and
+// action rows first, while the previous observation rows (the largest DMA group, issued
+// last by ctl_lds_load) are still in flight; then vel_cmd and the shift pass.
+template <bool TILE, class MID>
+__device__ __forceinline__ void ctl_assemble_split(const DevProgram &P, const CtlLds L, const CtlQ q, bool joy,
+                                                   int nrows, float *dst, int ds, float *raw, int tid, int nt,
+                                                   MID &&mid) {
+  unsigned nanm = 0u;
+  if (TILE && (q.pro.sub || q.pro.div || q.pro.mul)) {
+    ctl_append_noobs<TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    mid();
+    ctl_append_block<2, TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    GO2PI_STAMP(P, tid == 0, 50);
+    ctl_shift<TILE, true, 4>(L, q, nrows, dst, ds, raw, tid, nt);
+  } else {
+    ctl_append_noobs<TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    mid();
+    ctl_append_block<2, TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    GO2PI_STAMP(P, tid == 0, 50);
+    ctl_shift<TILE, false, 4>(L, q, nrows, dst, ds, raw, tid, nt);
+  }
+  ctl_nan_flush(L, nanm);
+  GO2PI_STAMP(P, tid == 0, 51);
+}
+
+// s_waitcnt vmcnt(n) for a run-time n (an immediate per case; n > 63 waits for 63)
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+#define GO2PI_VMW(i) \
+  case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    GO2PI_VMW(0) GO2PI_VMW(1) GO2PI_VMW(2) GO2PI_VMW(3) GO2PI_VMW(4) GO2PI_VMW(5) GO2PI_VMW(6) GO2PI_VMW(7)
+    GO2PI_VMW(8) GO2PI_VMW(9) GO2PI_VMW(10) GO2PI_VMW(11) GO2PI_VMW(12) GO2PI_VMW(13) GO2PI_VMW(14) GO2PI_VMW(15)
+    GO2PI_VMW(16) GO2PI_VMW(17) GO2PI_VMW(18) GO2PI_VMW(19) GO2PI_VMW(20) GO2PI_VMW(21) GO2PI_VMW(22) GO2PI_VMW(23)
+    GO2PI_VMW(24) GO2PI_VMW(25) GO2PI_VMW(26) GO2PI_VMW(27) GO2PI_VMW(28) GO2PI_VMW(29) GO2PI_VMW(30) GO2PI_VMW(31)
+#undef GO2PI_VMW
+    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+  }
+}
+
+// direct-to-LDS instructions glds_copy(n floats, this wave of nw) issues
+__device__ __forceinline__ int glds_count(int n, int wave, int nw) {
+  return n > wave * 64 ? (n - wave * 64 + nw * 64 - 1) / (nw * 64) : 0;
 }
 
 // What the final layer's store needs (controller tick), by value: the call's

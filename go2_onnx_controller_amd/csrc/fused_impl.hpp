@@ -1294,10 +1294,19 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     ctl_here = step == 0 && !P.has_gru;
     if (ctl_here) {
       const CtlQ cq = ctl_q(P, ctl);  // (its scalar loads land behind the barrier's wait)
-      wg_barrier_vm<RD * TPW>();
+      // r05: two waits. The direct-to-LDS loads went out as q0 | state, joystick and
+      // action rows | previous observation rows (ctl_lds_load) | the hidden biases, then
+      // the ring's fragments: the first wait lets this wave's observation, bias and ring
+      // loads stay in flight, so the blocks that need only the state / joystick / action
+      // rows are assembled while the observation rows land; the
+      // second (inside the assembly) waits for those before vel_cmd and the shift pass.
+      const int nrows = min(GO2PI_TILE_ROWS, B - row0);
+      const int later = glds_count(nrows * P.in_dim, wave, 4) + (step == 0 && !pre ? glds_count(hot.nbias, wave, 4) : 0);
+      vm_wait_rt(later + RD * TPW);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       GO2PI_STAMP(P, threadIdx.x == 0, 5);
-      ctl_assemble_flat<true>(P, CL, cq, ctl.joy != nullptr, min(GO2PI_TILE_ROWS, B - row0), X0, S,
-                              ctl.obs + (size_t)row0 * P.in_dim, threadIdx.x, 256);
+      ctl_assemble_split<true>(P, CL, cq, ctl.joy != nullptr, nrows, X0, S, ctl.obs + (size_t)row0 * P.in_dim,
+                               threadIdx.x, 256, [] { wg_barrier_vm<RD * TPW>(); });
       lds_barrier();
     }
   }
