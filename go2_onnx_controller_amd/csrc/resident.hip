@@ -1522,6 +1522,28 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
 struct A1Shape {
   int nl, h, f0;
 };
+
+// The generic act1 instantiations, by shape (AS run time, PRO, CW = 8; two sweeps in
+// flight, one where the weights leave no room for the second: act1_fits).
+template <int NL, int H, class GO>
+int a1_generic_f0(int f0, GO &go1) {
+  constexpr int D2 = (H == 128 && NL == 4) ? 1 : 2, D4 = (H == 128 && NL == 3) ? 1 : 2;
+  if (f0 == 1) return go1(policy_act1_kernel<NL, H, 1, 0xFFFFFFFFu, 2, true, 8>, 8);
+  if (f0 == 2) return go1(policy_act1_kernel<NL, H, 2, 0xFFFFFFFFu, D2, true, 8>, 8);
+  if constexpr (!(H == 128 && NL == 4)) return go1(policy_act1_kernel<NL, H, 4, 0xFFFFFFFFu, D4, true, 8>, 8);
+  return (int)hipErrorInvalidValue;  // (act1_shape refuses it)
+}
+template <class GO>
+int a1_generic(const A1Shape &a, GO &go1) {
+  if (a.h == 128) {
+    if (a.nl == 2) return a1_generic_f0<2, 128>(a.f0, go1);
+    if (a.nl == 3) return a1_generic_f0<3, 128>(a.f0, go1);
+    return a1_generic_f0<4, 128>(a.f0, go1);
+  }
+  if (a.nl == 2) return a1_generic_f0<2, 64>(a.f0, go1);
+  if (a.nl == 3) return a1_generic_f0<3, 64>(a.f0, go1);
+  return a1_generic_f0<4, 64>(a.f0, go1);
+}
 A1Shape act1_shape(const DevProgram &p) {
   A1Shape a{0, 0, 0};
   if (p.has_gru || p.nl < 2 || p.nl > 4 || p.L[p.nl - 1].N_pad != 16) return a;
@@ -1533,6 +1555,8 @@ A1Shape act1_shape(const DevProgram &p) {
   if (f0 == 3) f0 = 4;
   // (layer 0's lanes read their input row up to 64 F0: inside the row, zero past in_dim)
   if (f0 > 4 || p.lds_stride < std::max(64 * f0, H)) return a;
+  // weights per lane beyond the registers of 3 waves per SIMD (168): the r04 form
+  if (H == 128 && p.nl == 4 && f0 == 4) return a;
   a.nl = p.nl;
   a.h = H;
   a.f0 = f0;
@@ -1600,6 +1624,9 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
       if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false, 4>, 4);
       return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 2, false, 4>, 4);
     }
+    // every other act1 shape: activations and the prologue read at run time, two sweeps
+    // in flight, eight compute waves
+    return a1_generic(a1, go1);
   }
   if (p.nl == 4 && elu1 && r1_shape(p, 1024) == 0x2444u && r1_lgs(p, 1024) == 0x4333u)
     return go(policy_resident1_kernel<1024, R1_LMAX, 4, false, 0x2444u, 0x4333u, 0x0111u>, 1024);
