@@ -842,7 +842,15 @@ unsigned r1_lgs(const DevProgram &p, int nt) {
   return gs;
 }
 
+// the act1 shape of program p: {NL, H, F0}, or NL = 0 when it does not apply
+// (policy_act1_kernel below, r05)
+struct A1Shape {
+  int nl, h, f0;
+};
+A1Shape act1_shape(const DevProgram &p);
+
 bool resident1_fits(const DevProgram &p, bool ctl) {
+  if (act1_shape(p).nl && !std::getenv("GO2PI_RES_R1W")) return true;  // policy_act1_kernel (r05)
   const int nt = ctl ? 512 : 1024;
   // (nl >= 2: with one layer nothing would separate the request loop's top barrier from
   // the polling wave's next writes of st / x0)
@@ -1190,34 +1198,54 @@ __device__ __forceinline__ void a1_put(float *x0, int S, int in_dim, int B, int 
   x0[b * S + (f - b * in_dim)] = v;
 }
 
+// The controller form's granule i: the request's rows state [B][36] | joystick [B][5] |
+// previous observation [B][in_dim] | previous action [B][12] (engine.cpp resident_serve)
+// into the assembly's LDS image (ctl_fn.hpp CtlLds).
+__device__ __forceinline__ void a1_put_ctl(const CtlLds &L, int in_dim, int B, int i, float v) {
+  int f = i - 1;
+  const int ns = B * GO2PI_CTL_STATE_DIM, nj = B * GO2PI_CTL_JOY_DIM, no = B * in_dim;
+  if (f < ns) {
+    L.st[f] = v;
+    return;
+  }
+  f -= ns;
+  if (f < nj) {
+    L.jy[f] = v;
+    return;
+  }
+  f -= nj;
+  if (f < no) L.obs[f] = v;
+  else L.act[f - no] = v;
+}
+
 // The polling wave's wait for the next request. D sweeps of the header and the
-// observation granules in flight (pinned host memory, system scope), each checked when
-// it lands; the yield counter rides along with every sweep. 1: a request, its
-// observation rows (through the prologue) in x0; 0: leave (LEAVE header, idle bound,
-// moved yield counter, or a sweep that met a LEAVE granule). yield is never null (a
-// zero word stands in): a conditional load in the ring made the compiler wait for
-// every sweep in flight. v / yv: the sweep registers, owned by the caller and live
-// across its whole request loop, so that after a request is seen the sweeps still in
-// flight keep their registers: reused for the request word, the compiler made the
-// poller wait for them (~a PCIe round trip) before the staging barrier.
-template <int D, bool PRO>
-__device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned last, u64 idle_ticks, float *x0,
-                                       unsigned *err, int lane, unsigned &e, int &B, const unsigned *yield,
-                                       unsigned y0, const Pro &pro, const ProK (&pk)[A1_NP], u64 (&v)[D][A1_NP],
-                                       unsigned (&yv)[D]) {
+// request granules (NP loads per lane each) in flight (pinned host memory, system
+// scope), each checked when it lands; the yield counter rides along with every sweep.
+// 1: a request, its granules handed to put(i, value) (i = 1 .. B * per); 0: leave
+// (LEAVE header, idle bound, moved yield counter, or a sweep that met a LEAVE
+// granule). yield is never null (a zero word stands in): a conditional load in the
+// ring made the compiler wait for every sweep in flight. v / yv: the sweep registers,
+// owned by the caller and live across its whole request loop, so that after a request
+// is seen the sweeps still in flight keep their registers: reused for the request word,
+// the compiler made the poller wait for them (~a PCIe round trip) before the staging
+// barrier. put_k(i, value, k): the same for the sweep fallback, k = the column.
+template <int D, int NP, class PUT, class PUTK>
+__device__ __forceinline__ int a1_poll(const u64 *q, int per, unsigned last, u64 idle_ticks, unsigned *err, int lane,
+                                       unsigned &e, int &B, unsigned &word, const unsigned *yield, unsigned y0,
+                                       u64 (&v)[D][NP], unsigned (&yv)[D], PUT &&put, PUTK &&put_k) {
   u64 *qm = const_cast<u64 *>(q);
-  const int npoll = min(1 + in_dim, 64 * A1_NP);
+  const int npoll = min(1 + per, 64 * NP);
   // the previous call's sweeps, landed long ago: used here, so their registers stay
   // theirs until now
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     asm volatile("" ::"v"(yv[d]));
 #pragma unroll
-    for (int u = 0; u < A1_NP; ++u) asm volatile("" ::"v"(v[d][u]));
+    for (int u = 0; u < NP; ++u) asm volatile("" ::"v"(v[d][u]));
   }
   auto issue = [&](int d) {
 #pragma unroll
-    for (int u = 0; u < A1_NP; ++u)
+    for (int u = 0; u < NP; ++u)
       v[d][u] = __hip_atomic_load(qm + min(u * 64 + lane, npoll - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     yv[d] = __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
@@ -1232,29 +1260,26 @@ __device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned
       const unsigned tag = __builtin_amdgcn_readfirstlane((unsigned)(v[d][0] >> 32));
       if (tag == GO2PI_RES_LEAVE) return 0;
       if (tag != 0u && tag != last) {
-        const unsigned word = __builtin_amdgcn_readfirstlane((unsigned)v[d][0]);
+        word = __builtin_amdgcn_readfirstlane((unsigned)v[d][0]);
         B = min(max((int)(word & 0xFFu), 1), GO2PI_SMALL_MAXB);
-        const int n = B * in_dim;
+        const int n = B * per;
         if (1 + n <= npoll) {
           bool ok = true;
 #pragma unroll
-          for (int u = 0; u < A1_NP; ++u) {
+          for (int u = 0; u < NP; ++u) {
             const int i = u * 64 + lane;
             if (i >= 1 && i <= n) ok &= (unsigned)(v[d][u] >> 32) == tag;
           }
           if (__all(ok)) {
 #pragma unroll
-            for (int u = 0; u < A1_NP; ++u) {
+            for (int u = 0; u < NP; ++u) {
               const int i = u * 64 + lane;
-              if (i >= 1 && i <= n) {
-                const float x = __uint_as_float((unsigned)v[d][u]);
-                a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, pk[u], x) : x);
-              }
+              if (i >= 1 && i <= n) put(u, i, __uint_as_float((unsigned)v[d][u]));
             }
             e = tag;
             return 1;
           }
-        } else {  // more granules than one sweep holds (B > 1 with a wide observation)
+        } else {  // more granules than one sweep holds (B > 1 with a wide request)
           e = tag;
           for (unsigned spins = 0;; ++spins) {
             bool ok = true, lv = false;
@@ -1263,9 +1288,7 @@ __device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned
               const unsigned t = (unsigned)(g >> 32);
               ok &= t == tag;
               lv |= t == GO2PI_RES_LEAVE;
-              const int k = (i - 1) % in_dim;
-              const float x = __uint_as_float((unsigned)g);
-              a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, x, k) : x);
+              put_k(i, __uint_as_float((unsigned)g));
             }
             if (__any(lv)) return 0;
             if (__all(ok)) return 1;
@@ -1308,23 +1331,39 @@ __device__ __forceinline__ int a1_poll(const u64 *q, int in_dim, int S, unsigned
 // observation prologue (Sub / Div / Mul / Clip), applied by the polling wave. CW:
 // compute waves, 8 (two per SIMD, R = H / 32 outputs per lane) or 4 (one per SIMD,
 // R = H / 16: twice the weights per lane, half the lanes' reduction overhead).
-template <int NL, int H, int F0, unsigned AS, int D, bool PRO, int CW = 8>
+// CTL: the controller tick (go2pi_controller_step at batch <= 8; launch_resident's ctl
+// semantics): the request carries the tick's raw rows, which the polling wave puts
+// straight into the assembly's LDS image; the compute waves assemble the observation
+// (ctl_fn.hpp, the code of the batched kernel: the new rows go to the host staging, the
+// normalised ones to x0), run the layers, post-process the action into the staging
+// (ctl_store) and set the done word behind every output's drain.
+template <int NL, int H, int F0, unsigned AS, int D, bool PRO, int CW = 8, bool CTL = false>
 __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram *__restrict__ Pd, const u64 *req,
                                                                 u64 *actg, unsigned *err, unsigned *done,
-                                                                u64 idle_ticks, const unsigned *yield) {
+                                                                u64 idle_ticks, const unsigned *yield, DevCtl C) {
   static_assert(NL >= 2 && NL <= 4 && (H == 64 || H == 128) && F0 >= 1 && F0 <= 4 && (CW == 4 || CW == 8),
                 "policy_act1_kernel shape");
   constexpr int NT = a1_nt(CW);
   constexpr int R = H / (4 * CW);  // outputs per lane in a wide layer (a DPP row of 16 lanes: 16 R / 16)
   constexpr int HF = H / 64;  // float4s per lane of a K = H layer
   constexpr int NM = NL - 2 > 0 ? NL - 2 : 1;  // wide layers after layer 0 (array extent)
+  constexpr int NP = CTL ? 3 : A1_NP;          // granule loads per lane per sweep
+  // CTL: layer 0's weights live in LDS, not registers (re-read per request, 8 ds_read_b128
+  // per lane for the shipped model): beside the assembly's registers they spilled
+  constexpr bool W0L = CTL;
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
   const int S = P.lds_stride;
   float *x0 = reinterpret_cast<float *>(lds4);  // [8][S] layer 0's input rows (zero past in_dim)
   float *xa = x0 + GO2PI_SMALL_MAXB * S;        // [8][S] wide layers' rows (ping-pong)
   float *xb = xa + GO2PI_SMALL_MAXB * S;
-  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch
+  int *st = reinterpret_cast<int *>(xb + GO2PI_SMALL_MAXB * S);  // [0] leave, [1] epoch, [2] batch, [3] word
+  // CTL: the LDS image of the tick's inputs (q0 once, the request's rows per request),
+  // then layer 0's weights, lane-major [f][j][compute lane] float4 (a wave's read: 1 KiB
+  // contiguous)
+  const CtlLds CL = ctl_lds(reinterpret_cast<float *>(st + 4), GO2PI_SMALL_MAXB, P.in_dim);
+  float4 *w0l = reinterpret_cast<float4 *>(reinterpret_cast<float *>(st + 4) +
+                                           (CTL ? ctl_lds_floats(GO2PI_SMALL_MAXB, P.in_dim) : 0));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = tid - 64;                // compute lane (the polling wave: negative)
@@ -1370,55 +1409,83 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
     for (int f = 0; f < HF; ++f) wo[f] = hl ? wld(L, grp, 64 * f + 4 * s) : z4;
     if (hl) bo = L.bias[grp];
   }
-  // the program fields a request reads, in SGPRs for the kernel's life
+  // the program fields a request reads, in SGPRs for the kernel's life (run-time
+  // activations). With the activations compiled in (AS) the launcher has checked the
+  // hidden layers' Elu alpha is 1 and the head has none, and the post-processing
+  // fields are left to the compiler: pinned in SGPRs beside the controller form's
+  // parameters they spilled 63 SGPRs into VGPR lanes, and those to scratch.
+  constexpr bool ACT_RT = AS == 0xFFFFFFFFu;
   int lact[NL];
   float lal[NL], lbe[NL];
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
-    lact[l] = r1_keep(P.L[l].act);
-    lal[l] = r1_keep(P.L[l].alpha);
-    lbe[l] = r1_keep(P.L[l].beta);
+    lact[l] = ACT_RT ? r1_keep(P.L[l].act) : 0;
+    lal[l] = ACT_RT ? r1_keep(P.L[l].alpha) : 1.f;
+    lbe[l] = ACT_RT ? r1_keep(P.L[l].beta) : 0.f;
   }
-  const int post_tanh = r1_keep(P.post_tanh);
-  const float clo = r1_keep(P.clip_lo), chi = r1_keep(P.clip_hi), pscale = r1_keep(P.scale);
+  const int post_tanh = ACT_RT ? r1_keep(P.post_tanh) : P.post_tanh;
+  const float clo = ACT_RT ? r1_keep(P.clip_lo) : P.clip_lo, chi = ACT_RT ? r1_keep(P.clip_hi) : P.clip_hi;
+  const float pscale = ACT_RT ? r1_keep(P.scale) : P.scale;
   // the polling wave: each lane's prologue constants for its granule positions (the
   // column of granule i is (i - 1) mod in_dim whatever the batch)
   const Pro pro = PRO ? pro_of(P) : Pro{};
-  ProK pk[A1_NP];
+  ProK pk[NP];
 #pragma unroll
-  for (int u = 0; u < A1_NP; ++u) {
+  for (int u = 0; u < NP; ++u) {
     const int i = u * 64 + lane;
     pk[u] = (PRO && wave == 0 && i >= 1) ? pro_k(pro, (i - 1) % in_dim) : ProK{0.f, 1.f, 1.f};
   }
   for (int i = tid; i < GO2PI_SMALL_MAXB * S; i += NT) x0[i] = 0.f;
+  if constexpr (W0L) {
+    if (c >= 0)
+#pragma unroll
+      for (int f = 0; f < F0; ++f)
+#pragma unroll
+        for (int j = 0; j < R; ++j) w0l[(f * R + j) * 64 * CW + c] = w0[f][j];
+  }
+  if constexpr (CTL) {
+    if (tid < 2 * GO2PI_CTL_DOF) reinterpret_cast<float *>(CL.q0)[tid] = reinterpret_cast<const float *>(C.prm->q0)[tid];
+    if (tid < GO2PI_TILE_ROWS) CL.nanf[tid] = 0u;
+  }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): weights and constants in registers before the first wait
   const unsigned y0 = __hip_atomic_load(const_cast<unsigned *>(yield), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // x0 cleared before the poller writes a row into it
   unsigned last = 0, nreq = 0;
   (void)nreq;
-  u64 pv[D][A1_NP];  // the polling wave's sweep registers (a1_poll)
+  u64 pv[D][NP];  // the polling wave's sweep registers (a1_poll)
   unsigned pyv[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     pyv[d] = 0u;
 #pragma unroll
-    for (int u = 0; u < A1_NP; ++u) pv[d][u] = 0ull;
+    for (int u = 0; u < NP; ++u) pv[d][u] = 0ull;
   }
+  const int per = CTL ? GO2PI_CTL_RAW + in_dim : in_dim;  // request floats per robot
   for (;;) {
     if (wave == 0) {
-      unsigned e = 0;
+      unsigned e = 0, word = 0;
       int B = 1;
-      const int got =
-          a1_poll<D, PRO>(req, in_dim, S, last, idle_ticks, x0, err, lane, e, B, yield, y0, pro, pk, pv, pyv);
+      int got;
+      if constexpr (CTL) {
+        got = a1_poll<D, NP>(req, per, last, idle_ticks, err, lane, e, B, word, yield, y0, pv, pyv,
+                             [&](int, int i, float x) { a1_put_ctl(CL, in_dim, B, i, x); },
+                             [&](int i, float x) { a1_put_ctl(CL, in_dim, B, i, x); });
+      } else {
+        got = a1_poll<D, NP>(
+            req, per, last, idle_ticks, err, lane, e, B, word, yield, y0, pv, pyv,
+            [&](int u, int i, float x) { a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, pk[u], x) : x); },
+            [&](int i, float x) { a1_put(x0, S, in_dim, B, i, PRO ? prologue(pro, x, (i - 1) % in_dim) : x); });
+      }
       A1_STAMP(0, 0);
       A1_CLOCK(0, 15);
       if (lane == 0) {
         st[0] = !got;
         st[1] = (int)e;
         st[2] = B;
+        st[3] = (int)word;
       }
     }
-    lds_barrier();  // the request's rows are in x0
+    lds_barrier();  // the request's rows are in x0 (CTL: in the assembly's image)
     // (row 0's layer-0 input read beside the request word: one LDS round trip, not two)
     float4 xpre[F0];
 #pragma unroll
@@ -1427,12 +1494,28 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
     if (sv.x) break;
     const unsigned e = (unsigned)sv.y;
     const int B = sv.z;
+    const unsigned word = (unsigned)sv.w;
     last = e;
-    if (wave == 0) {  // the poller passes the layers' barriers, then polls again
+    if (wave == 0) {  // the poller passes the request's barriers, then polls again
 #pragma unroll
       for (int l = 0; l + 1 < NL; ++l) lds_barrier();
+      if constexpr (CTL) {
+        lds_barrier();  // the assembly
+        lds_barrier();  // the outputs drained (the done word)
+      }
       ++nreq;
       continue;
+    }
+    CtlView cv{};
+    if constexpr (CTL) {
+      // the observation assembled from the image: the new rows to the host staging, their
+      // normalised values to x0 (the padding rows past B, which it zero-fills, reach into
+      // xa: written by layer 0 before any read)
+      const bool joy = (word & GO2PI_RES_JOY) != 0u;
+      ctl_assemble_flat<true, 2>(P, CL, ctl_q(P, C), joy, B, x0, S, C.obs, c, 64 * CW);
+      lds_barrier();
+#pragma unroll
+      for (int f = 0; f < F0; ++f) xpre[f] = *reinterpret_cast<const float4 *>(x0 + 64 * f + 4 * s);
     }
     A1_STAMP(64, 1);
     A1_CLOCK(64, 13);
@@ -1452,8 +1535,9 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
             const float4 x = b == 0 ? xpre[f] : *reinterpret_cast<const float4 *>(xr + 64 * f);
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-              acc[j] = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{w0[f][j].x, w0[f][j].y}, acc[j]);
-              acc[j] = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{w0[f][j].z, w0[f][j].w}, acc[j]);
+              const float4 wv = W0L ? w0l[(f * R + j) * 64 * CW + c] : w0[f][j];
+              acc[j] = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{wv.x, wv.y}, acc[j]);
+              acc[j] = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{wv.z, wv.w}, acc[j]);
             }
           }
         } else {
@@ -1484,6 +1568,14 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       Y = Y == xa ? xb : xa;
     }
     // ---- the head: 16 outputs, one per DPP row of compute waves 0..3
+    if constexpr (CTL) {  // (the outputs' view formed here: live across the layers, its fields spilled)
+      DevCtl cc = C;
+      if (!(word & GO2PI_RES_JOY)) cc.joy = nullptr;
+      if (!(word & GO2PI_RES_QDES)) cc.q_des = nullptr;
+      if (!(word & GO2PI_RES_KP)) cc.kp = nullptr;
+      if (!(word & GO2PI_RES_KD)) cc.kd = nullptr;
+      cv = ctl_view(cc, CL, 0);
+    }
     if (c < 256) {
       const int A = AS != 0xFFFFFFFFu ? (int)((AS >> (4 * (NL - 1))) & 15u) : lact[NL - 1];
       for (int b = 0; b < B; ++b) {
@@ -1501,13 +1593,32 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
           float y = act_fn(A, lal[NL - 1], lbe[NL - 1], v + bo);
           if (post_tanh) y = tanhf(y);
           y = clip_nan(y, clo, chi) * pscale;
-          __hip_atomic_store(actg + (size_t)b * nout + grp, ((u64)e << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+          if constexpr (CTL) {
+            int n = grp;
+            asm volatile("" : "+v"(n));  // (per-lane output addresses formed here, not hoisted and spilled)
+            ctl_store(cv, b, n, y);
+          } else {
+            int n = grp;
+            asm volatile("" : "+v"(n));  // (the granule address formed here, not hoisted and spilled)
+            __hip_atomic_store(actg + (size_t)b * nout + n, ((u64)e << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          }
         }
       }
     }
     A1_STAMP(64, 8);
     A1_CLOCK(64, 14);
+    if constexpr (CTL) {  // the NaN flags, every output drained, then the done word
+      if ((word & GO2PI_RES_STATUS) && c < B) {
+        int cs = c;
+        asm volatile("" : "+v"(cs));  // (the address formed here, not hoisted and spilled)
+        C.status[cs] = CL.nanf[cs];
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      if (c < GO2PI_TILE_ROWS) CL.nanf[c] = 0u;  // (read above, before the barrier)
+      if (c == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     ++nreq;
   }
   // leaving: every wave's answer stores (and the poller's sweeps) drained before the
@@ -1518,10 +1629,6 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
   if (tid == 0) __hip_atomic_store(done, GO2PI_RES_LEAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// the act1 shape of program p: {NL, H, F0}, or NL = 0 when it does not apply
-struct A1Shape {
-  int nl, h, f0;
-};
 
 // The generic act1 instantiations, by shape (AS run time, PRO, CW = 8; two sweeps in
 // flight, one where the weights leave no room for the second: act1_fits).
@@ -1532,6 +1639,25 @@ int a1_generic_f0(int f0, GO &go1) {
   if (f0 == 2) return go1(policy_act1_kernel<NL, H, 2, 0xFFFFFFFFu, D2, true, 8>, 8);
   if constexpr (!(H == 128 && NL == 4)) return go1(policy_act1_kernel<NL, H, 4, 0xFFFFFFFFu, D4, true, 8>, 8);
   return (int)hipErrorInvalidValue;  // (act1_shape refuses it)
+}
+// ... and of the controller form (the assembly applies the prologue: PRO false; D = 1)
+template <int NL, int H, class GO>
+int a1_generic_ctl_f0(int f0, GO &go1) {
+  if (f0 == 1) return go1(policy_act1_kernel<NL, H, 1, 0xFFFFFFFFu, 1, false, 8, true>, 8);
+  if (f0 == 2) return go1(policy_act1_kernel<NL, H, 2, 0xFFFFFFFFu, 1, false, 8, true>, 8);
+  if constexpr (!(H == 128 && NL == 4)) return go1(policy_act1_kernel<NL, H, 4, 0xFFFFFFFFu, 1, false, 8, true>, 8);
+  return (int)hipErrorInvalidValue;  // (act1_shape refuses it)
+}
+template <class GO>
+int a1_generic_ctl(const A1Shape &a, GO &go1) {
+  if (a.h == 128) {
+    if (a.nl == 2) return a1_generic_ctl_f0<2, 128>(a.f0, go1);
+    if (a.nl == 3) return a1_generic_ctl_f0<3, 128>(a.f0, go1);
+    return a1_generic_ctl_f0<4, 128>(a.f0, go1);
+  }
+  if (a.nl == 2) return a1_generic_ctl_f0<2, 64>(a.f0, go1);
+  if (a.nl == 3) return a1_generic_ctl_f0<3, 64>(a.f0, go1);
+  return a1_generic_ctl_f0<4, 64>(a.f0, go1);
 }
 template <class GO>
 int a1_generic(const A1Shape &a, GO &go1) {
@@ -1599,7 +1725,11 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
   // sweeps in flight, 1 / 2 / 4)
   const A1Shape a1 = act1_shape(p);
   if (a1.nl && !std::getenv("GO2PI_RES_R1W")) {
-    const size_t lds1 = sizeof(float) * (3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4);
+    // (the controller form: the assembly's image and layer 0's weights, lane-major, besides)
+    const size_t lds1 = sizeof(float) * (3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 +
+                                         (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) +
+                                                    (size_t)a1.f0 * (a1.h / 32) * 512 * 4
+                                              : 0));
     auto go1 = [&](auto kern, int cw) {
       if (lds1 > 64 * 1024) {
         const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -1608,7 +1738,8 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
       }
       // (yield never null: the kernel loads it unconditionally, see a1_poll)
       hipLaunchKernelGGL(kern, dim3(1), dim3(a1_nt(cw)), lds1, reinterpret_cast<hipStream_t>(stream), p_dev, req, actg,
-                         err, done, idle_ticks, yield ? yield : reinterpret_cast<const unsigned *>(p.zero));
+                         err, done, idle_ticks, yield ? yield : reinterpret_cast<const unsigned *>(p.zero),
+                         ctl ? *ctl : DevCtl{});
       return (int)hipGetLastError();
     };
     const char *dv = std::getenv("GO2PI_A1_DEPTH");
@@ -1616,6 +1747,11 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
     const bool pro = p.pre_sub || p.pre_div || p.pre_mul || p.pre_clip;
     const char *cv = std::getenv("GO2PI_A1_CW");
     const int cw = cv && std::atoi(cv) == 4 ? 4 : 8;
+    if (ctl) {  // the controller form: one sweep in flight (three loads per lane), eight compute waves
+      if (a1.nl == 4 && a1.h == 128 && a1.f0 == 2 && elu1)
+        return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false, 8, true>, 8);
+      return a1_generic_ctl(a1, go1);
+    }
     if (a1.nl == 4 && a1.h == 128 && a1.f0 == 2 && elu1 && !pro) {
       if (cw == 8) {
         if (depth == 1) return go1(policy_act1_kernel<4, 128, 2, 0x0111u, 1, false, 8>, 8);

@@ -70,11 +70,14 @@ def test_controller_long_closed_loop_no_joystick():
 
 
 @pytest.mark.parametrize("name,hist", [("ctl_h1", 1), ("ctl_h3", 3), ("ctl_h16", 16)])
-@pytest.mark.parametrize("B", [5, 300])
-def test_controller_history_lengths(synth_path, name, hist, B):
+@pytest.mark.parametrize("B,res", [(5, 0), (5, 500), (300, 0)])
+def test_controller_history_lengths(synth_path, name, hist, B, res):
+    """Other history lengths (49 x kHistory observations): B = 5 by one launch per tick or
+    by the resident kernel's controller form (the generic policy_act1_kernel shapes for
+    ctl_h1 and ctl_h3, the multi-workgroup form for ctl_h16), and the batched kernel."""
     from go2_onnx_controller_amd import Engine
     p = synth_path(name)
-    with Engine(p, max_batch=B) as e:
+    with Engine(p, max_batch=B, resident_ms=res) as e:
         assert e.ctl_history() == hist
         _run_ticks(e, _mlp_policy(p), B, 3, seed=B + hist, hist=hist)
 
@@ -178,18 +181,21 @@ def test_controller_rejects_non_controller_policy(synth_path):
                               np.zeros((1, 12), np.float32))
 
 
-@pytest.mark.parametrize("form", ["one", "multi"])
+@pytest.mark.parametrize("form", ["one", "one_r1w", "multi"])
 @pytest.mark.parametrize("B", [1, 3, 8])
 def test_controller_ticks_resident(B, form, monkeypatch):
     """The resident kernel's controller form (go2pi_opts.resident_ms > 0, batch <= 8):
     same bit-exact observation / action contract, with and without joystick rows,
     with and without the optional outputs, and switching to and from the act() form.
-    form: the single-workgroup kernel (the shipped model's default) or the
+    form: the single-workgroup kernel (the shipped model's default: r05's polling-wave
+    policy_act1_kernel, or r04's 512-thread form with GO2PI_RES_R1W=1) or the
     multi-workgroup one (GO2PI_RES_MULTI=1)."""
     from go2_onnx_controller_amd import Engine
     from oracle import controller_ref as cr
     if form == "multi":
         monkeypatch.setenv("GO2PI_RES_MULTI", "1")
+    elif form == "one_r1w":
+        monkeypatch.setenv("GO2PI_RES_R1W", "1")
     pol = _mlp_policy(SHIPPED)
     with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
         obs, act = _run_ticks(e, pol, B, 6, seed=40 + B)
@@ -204,12 +210,14 @@ def test_controller_ticks_resident(B, form, monkeypatch):
             assert rel_err(e.run(x), pol(x)) <= TOL
 
 
-@pytest.mark.parametrize("form", ["one", "multi"])
+@pytest.mark.parametrize("form", ["one", "one_r1w", "multi"])
 def test_controller_resident_nan_status(form, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import controller_ref as cr
     if form == "multi":
         monkeypatch.setenv("GO2PI_RES_MULTI", "1")
+    elif form == "one_r1w":
+        monkeypatch.setenv("GO2PI_RES_R1W", "1")
     rng = np.random.default_rng(77)
     B = 4
     with Engine(SHIPPED, max_batch=8, resident_ms=500) as e:
