@@ -25,7 +25,11 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
+
+#include <immintrin.h>
+#include <sys/mman.h>
 
 #include "../../include/go2pi.h"
 #include "onnx_model.hpp"
@@ -86,6 +90,63 @@ void *pin_take(size_t &bytes) {
 void pin_give(void *p, size_t bytes) {
   std::lock_guard<std::mutex> lk(g_pin_mu);
   g_pin_free.emplace_back(bytes, p);
+}
+
+// The resident kernels' request ring in fine-grained device memory that the host
+// writes through its large-BAR mapping of VRAM: a request then reaches the polling
+// wave as posted PCIe writes into the GPU's own memory, instead of the wave reading
+// pinned host memory across PCIe (a read round trip per poll). tools/bar_probe.hip,
+// profiles/r05_bar_probe.txt: live-kernel host -> GPU -> host round trip p50 1.78 us
+// against 2.47 us. Whether an allocation is mapped into the host's address space is
+// checked with msync() on its pages, never by touching it; without large BAR the ring
+// stays in pinned host memory (GO2PI_REQ_HOST=1 forces that, for A/B). Like pinned
+// blocks, these are never freed (hipFree synchronises the device): cached per device.
+std::vector<std::tuple<int, size_t, void *>> g_bar_free;  // (device, bytes, block), under g_pin_mu
+std::vector<int> g_bar_absent;                            // devices whose VRAM the host cannot map
+
+bool host_mapped(const void *p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
+  const size_t n = ((reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095)) - a;
+  return msync(reinterpret_cast<void *>(a), n, MS_ASYNC) == 0;
+}
+
+// a host-writable device block of at least `bytes` (out: its size) on the current
+// device `device`, zeroed; nullptr when the host cannot map this device's memory
+void *bar_take(int device, size_t &bytes) {
+  bytes = (bytes + 4095) & ~(size_t)4095;
+  if (std::getenv("GO2PI_REQ_HOST")) return nullptr;
+  void *p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (std::find(g_bar_absent.begin(), g_bar_absent.end(), device) != g_bar_absent.end()) return nullptr;
+    for (size_t i = 0; i < g_bar_free.size(); ++i)
+      if (std::get<0>(g_bar_free[i]) == device && std::get<1>(g_bar_free[i]) >= bytes) {
+        bytes = std::get<1>(g_bar_free[i]);
+        p = std::get<2>(g_bar_free[i]);
+        g_bar_free.erase(g_bar_free.begin() + (long)i);
+        break;
+      }
+  }
+  if (!p) {
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+    }
+    if (!p || !host_mapped(p, bytes)) {
+      std::lock_guard<std::mutex> lk(g_pin_mu);
+      g_bar_absent.push_back(device);
+      if (p) g_bar_free.emplace_back(device, bytes, p);  // (kept: hipFree would synchronise the device)
+      return nullptr;
+    }
+  }
+  std::memset(p, 0, bytes);  // (through the mapping: a reused ring holds another engine's tags)
+  _mm_sfence();
+  return p;
+}
+
+void bar_give(int device, void *p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_bar_free.emplace_back(device, bytes, p);
 }
 
 // Every entry point leaves the calling thread's current HIP device as it found it
@@ -151,7 +212,8 @@ struct go2pi_engine {
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
-  unsigned long long *h_req = nullptr, *m_req = nullptr;  // host-mapped request granules
+  unsigned long long *h_req = nullptr, *m_req = nullptr;  // request granules: host view, device view
+  size_t req_bar_bytes = 0;  // > 0: the ring is in device memory the host writes through the BAR (bar_take)
   unsigned long long *d_mirror = nullptr;                 // device copy of the request (workgroup 0 -> the rest)
   unsigned long long res_idle_ticks = 0;                  // 100 MHz wall-clock ticks
   std::chrono::steady_clock::time_point res_last{};
@@ -180,6 +242,7 @@ struct go2pi_engine {
     }
     for (void *p : allocs) (void)hipFreeAsync(p, stream);
     for (auto &b : pinned) pin_give(b.second, b.first);
+    if (req_bar_bytes) bar_give(device, h_req, req_bar_bytes);
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -345,6 +408,7 @@ struct go2pi_engine {
         __atomic_store_n(h_req + 1 + i, ((unsigned long long)e0 << 32) | bits, __ATOMIC_RELAXED);
       }
       __atomic_store_n(h_req, ((unsigned long long)e0 << 32) | (unsigned)batch | flags, __ATOMIC_RELEASE);
+      if (req_bar_bytes) _mm_sfence();  // the BAR mapping is write-combined: send the request now
       const auto t0 = std::chrono::steady_clock::now();
       unsigned d;
       if (ctl) {  // the controller form: a done word behind the drained outputs
@@ -846,7 +910,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     if ((e.latency_ok || res_rnn) && e.done_ok && e.opts.resident_ms > 0) {
       // room for a controller tick's rows too (GO2PI_CTL_RAW + in_dim floats per robot)
       const size_t nreq = 1 + GO2PI_SMALL_MAXB * (size_t)(m.in_dim + GO2PI_CTL_RAW);
-      e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
+      size_t rb = sizeof(unsigned long long) * nreq;
+      if (void *bar = bar_take(e.device, rb)) {  // large BAR: the ring in VRAM, written by the host
+        e.h_req = e.m_req = static_cast<unsigned long long *>(bar);
+        e.req_bar_bytes = rb;
+      } else {
+        e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
+      }
       e.palloc(&e.h_actg, &e.m_actg, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)m.out_dim);
       e.d_mirror = e.dalloc<unsigned long long>(1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim);
       int khz = 0;

@@ -441,14 +441,16 @@ def test_small_batched_launch_beside_busy_resident_kernel(synth_path):
     xb = torch.randn((1024, 48), device="cuda:0")
     s = torch.cuda.Stream()
 
-    def timed(b, n=40):
-        ts = []
-        for _ in range(n):
+    def timed(b, n=40, until=None):
+        # n launches; with `until`, launches continue (within 3 s) until it holds
+        ts, t_end = [], time.perf_counter() + 3.0
+        while len(ts) < n or (until is not None and not until() and time.perf_counter() < t_end):
             t0 = time.perf_counter()
             yb = b.run_torch(xb, stream=s)
             s.synchronize()
             ts.append(time.perf_counter() - t0)
-        return sorted(ts)[n // 2], yb
+            time.sleep(0.0002)
+        return sorted(ts)[len(ts) // 2], yb
     errs, n_act = [], [0]
     stop = threading.Event()
     with Engine(pb, max_batch=4096) as b:
@@ -470,7 +472,7 @@ def test_small_batched_launch_beside_busy_resident_kernel(synth_path):
             th = threading.Thread(target=tick)
             th.start()
             try:
-                busy, yb = timed(b)
+                busy, yb = timed(b, until=lambda: n_act[0] >= 20)
             finally:
                 stop.set()
                 th.join(timeout=10)
