@@ -1618,6 +1618,7 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       lds_barrier();
       if (c < GO2PI_TILE_ROWS) CL.nanf[c] = 0u;  // (read above, before the barrier)
       if (c == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      A1_STAMP(64, 9);
     }
     ++nreq;
   }

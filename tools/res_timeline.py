@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--model", default="go2_mlp_512")
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "res_timeline.json"))
+    ap.add_argument("--ctl", action="store_true",
+                    help="time the controller tick (go2pi_controller_step, batch 1) instead of act()")
     ap.add_argument("--form", choices=["multi", "one"], default="multi",
                     help="the resident kernel the engine runs: multi-workgroup (policy_resident_kernel) or the "
                          "single-workgroup policy_resident1_kernel (r04; GO2PI_RES_MULTI=1 forces multi)")
@@ -52,10 +54,16 @@ def main():
         x = np.random.default_rng(2).standard_normal((1, e.in_dim)).astype(np.float32)
         y = np.empty((1, e.out_dim), np.float32)
         ts = []
+        st = np.zeros((1, 36), np.float32)
+        st[0, 0] = 1.0
         for i in range(args.iters):
             x[0, i % e.in_dim] += 1e-3
             t0 = time.perf_counter_ns()
-            e.run_ptr(x.ctypes.data, y.ctypes.data, 1)
+            if args.ctl:
+                st[0, 7 + i % 12] += 1e-3
+                e.controller_step(st, x, y)
+            else:
+                e.run_ptr(x.ctypes.data, y.ctypes.data, 1)
             ts.append((time.perf_counter_ns() - t0) / 1e3)
         st = e.diag_stamps(512 * 32).astype(np.int64).reshape(512, 32)  # syncs: waits for the idle exit
     ts.sort()
@@ -97,7 +105,7 @@ def one_workgroup(args, st, ts, np):
     layers), 8 the answer's granule stores issued (wave 1's head output)."""
     rows = st[(st[:, 0] > 0) & (st[:, 8] > 0)]
     rel = (rows - rows[:, 0:1]) * 10.0 / 1e3
-    names = {1: "input staged", 8: "answer issued"}
+    names = {1: "input staged", 8: "answer issued", 9: "done word (controller form)"}
     for l in range(6):
         names[2 + l] = f"layer{l} done"
     med, prev = {}, 0.0
