@@ -1700,9 +1700,9 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
                      const unsigned *yield, const DevCtl *ctl, void *stream) {
   if (!resident1_fits(p, ctl != nullptr)) return (int)hipErrorInvalidValue;
-  const size_t lds = resident1_lds_bytes(p, ctl != nullptr);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const size_t lds = resident1_lds_bytes(p, ctl != nullptr);  // (r04's forms)
   auto go = [&](auto kern, int nt) {
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     if (lds > 64 * 1024) {
       const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1716,11 +1716,6 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
   // instantiation: the registers it leaves free keep the controller form out of scratch
   // (Elu alpha 1 on the hidden layers, no activation on the head: the exported policy's)
   const bool elu1 = r1_acts(p) == 0x0111u && p.L[0].alpha == 1.f && p.L[1].alpha == 1.f && p.L[2].alpha == 1.f;
-  if (ctl) {
-    if (p.nl == 4 && elu1 && r1_shape(p, 512) == 0x2887u && r1_lgs(p, 512) == 0x4222u)
-      return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x2887u, 0x4222u, 0x0111u>, 512);
-    return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x8888u>, 512);
-  }
   // r05: the polling-wave form (policy_act1_kernel) wherever its shape applies
   // (GO2PI_RES_R1W=1: the r04 1024-thread form, A/B diagnostics; GO2PI_A1_DEPTH: poll
   // sweeps in flight, 1 / 2 / 4)
@@ -1764,6 +1759,11 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
     // every other act1 shape: activations and the prologue read at run time, two sweeps
     // in flight, eight compute waves
     return a1_generic(a1, go1);
+  }
+  if (ctl) {  // r04's forms
+    if (p.nl == 4 && elu1 && r1_shape(p, 512) == 0x2887u && r1_lgs(p, 512) == 0x4222u)
+      return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x2887u, 0x4222u, 0x0111u>, 512);
+    return go(policy_resident1_kernel<512, R1_LMAX, 8, true, 0x8888u>, 512);
   }
   if (p.nl == 4 && elu1 && r1_shape(p, 1024) == 0x2444u && r1_lgs(p, 1024) == 0x4333u)
     return go(policy_resident1_kernel<1024, R1_LMAX, 4, false, 0x2444u, 0x4333u, 0x0111u>, 1024);
