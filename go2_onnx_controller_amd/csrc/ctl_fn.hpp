@@ -258,13 +258,37 @@ __device__ __forceinline__ void ctl_append(const CtlLds L, const CtlQ &q, bool j
   ctl_nan_flush(L, nanm);
 }
 
+// ctl_append with one wave per block (waves 0..6 of the caller's nt = 64 * nw >= 448
+// threads; tid: the caller's thread index): every branch wave-uniform, and the seven
+// blocks' LDS round trips overlap across waves instead of following one another in every
+// thread (the batch-1 resident kernel: ~1.5K cycles as ctl_append, seven dependent
+// round trips per thread).
+template <bool TILE, bool ARITH>
+__device__ __forceinline__ void ctl_append_waves(const CtlLds L, const CtlQ &q, bool joy, int nrows,
+                                                 float *__restrict__ dst, int ds, float *__restrict__ raw, int tid) {
+  unsigned nanm = 0u;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  switch (w) {
+    case 0: ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 1: ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 2: ctl_append_block<2, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 3: ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 4: ctl_append_block<4, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 5: ctl_append_block<5, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    case 6: ctl_append_block<6, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+    default: break;
+  }
+  ctl_nan_flush(L, nanm);
+}
+
 // The shifted values (std::shift_left by d, controller.hpp:45-52): column k of
 // every row r < nrows takes the image's column k + d. The (H - 1) * 49 shifted
 // columns of all rows are one flat range (row-major, so a wave's reads and the
 // caller's row stores are contiguous), U elements per thread in flight: every LDS
 // read issued before the first store. TILE: dst is the batched kernel's LDS tile
-// — its padding columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too.
-template <bool TILE, bool ARITH, int U>
+// — its padding columns [in_dim, in_pad) and rows [nrows, 16) are zeroed too, unless
+// PAD is false (a caller whose padding stays zero and whose rows past nrows are never read).
+template <bool TILE, bool ARITH, int U, bool PAD = TILE>
 __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nrows, float *__restrict__ dst, int ds,
                                           float *__restrict__ raw, int tid, int nt) {
   const float *__restrict__ obs_l = L.obs;
@@ -294,7 +318,7 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nro
       dst[rr[u] * ds + kk[u]] = ctl_pro<TILE, ARITH>(q, x[u], kk[u]);
     }
   }
-  if constexpr (TILE) {
+  if constexpr (TILE && PAD) {
     const int pw = q.in_pad - in_dim;
     for (int e = tid; e < nrows * pw; e += nt) {
       const int r = e / pw;

@@ -1348,8 +1348,9 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
   constexpr int HF = H / 64;  // float4s per lane of a K = H layer
   constexpr int NM = NL - 2 > 0 ? NL - 2 : 1;  // wide layers after layer 0 (array extent)
   constexpr int NP = CTL ? 3 : A1_NP;          // granule loads per lane per sweep
-  // CTL: layer 0's weights live in LDS, not registers (re-read per request, 8 ds_read_b128
-  // per lane for the shipped model): beside the assembly's registers they spilled
+  // CTL: layer 0's and the head's weights live in LDS, not registers (re-read per request,
+  // 8 + 2 ds_read_b128 per lane for the shipped model): beside the assembly's registers
+  // they spilled
   constexpr bool W0L = CTL;
   const DevProgram &P = *Pd;
   extern __shared__ float4 lds4[];
@@ -1364,6 +1365,10 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
   const CtlLds CL = ctl_lds(reinterpret_cast<float *>(st + 4), GO2PI_SMALL_MAXB, P.in_dim);
   float4 *w0l = reinterpret_cast<float4 *>(reinterpret_cast<float *>(st + 4) +
                                            (CTL ? ctl_lds_floats(GO2PI_SMALL_MAXB, P.in_dim) : 0));
+  // CTL: the head's weights too (lane-major [f][head lane], 256 lanes), then the request's
+  // new observation rows [B][in_dim]
+  float4 *wol = w0l + (W0L ? F0 * R * 64 * CW : 0);
+  float *obsn = reinterpret_cast<float *>(wol + (W0L ? HF * 256 : 0));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = tid - 64;                // compute lane (the polling wave: negative)
@@ -1442,6 +1447,9 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       for (int f = 0; f < F0; ++f)
 #pragma unroll
         for (int j = 0; j < R; ++j) w0l[(f * R + j) * 64 * CW + c] = w0[f][j];
+    if (c >= 0 && c < 256)
+#pragma unroll
+      for (int f = 0; f < HF; ++f) wol[f * 256 + c] = wo[f];
   }
   if constexpr (CTL) {
     if (tid < 2 * GO2PI_CTL_DOF) reinterpret_cast<float *>(CL.q0)[tid] = reinterpret_cast<const float *>(C.prm->q0)[tid];
@@ -1508,11 +1516,39 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
     }
     CtlView cv{};
     if constexpr (CTL) {
-      // the observation assembled from the image: the new rows to the host staging, their
-      // normalised values to x0 (the padding rows past B, which it zero-fills, reach into
-      // xa: written by layer 0 before any read)
+      A1_STAMP(64, 10);
+      // the observation assembled from the image: the new rows to LDS (obsn; they go to the
+      // host staging with the other outputs after the head), their normalised values to x0
+      // (the padding rows past B, which it zero-fills, reach into xa: written by layer 0
+      // before any read). Stored straight to the host staging here, the rows' PCIe stores
+      // sat in front of every later wait of the request.
+      A1_CLOCK(64, 11);
       const bool joy = (word & GO2PI_RES_JOY) != 0u;
-      ctl_assemble_flat<true, 2>(P, CL, ctl_q(P, C), joy, B, x0, S, C.obs, c, 64 * CW);
+      const CtlQ q = ctl_q(P, C);
+#ifdef GO2PI_DIAG_RESCLK
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the parameters' arrival timed on its own)
+#endif
+      A1_CLOCK(64, 19);
+      // (ctl_assemble_flat's two passes, timed apart: shader-clock slots 19-21)
+      // (x0's padding columns stay zero from the start and its rows past B are never read:
+      // the shift pass leaves them alone)
+      static_assert(CW >= 7, "the controller form's assembly runs one history block per compute wave");
+      if (q.pro.sub || q.pro.div || q.pro.mul) {
+        ctl_append_waves<true, true>(CL, q, joy, B, x0, S, obsn, c);
+        A1_CLOCK(64, 20);
+        ctl_shift<true, true, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+      } else {
+        ctl_append_waves<true, false>(CL, q, joy, B, x0, S, obsn, c);
+        A1_CLOCK(64, 20);
+        ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+      }
+      A1_CLOCK(64, 21);
+#ifdef GO2PI_DIAG_ASM2  // both passes again, warm (instruction fetch and first touches vs. work): slots 22-23
+      ctl_append_waves<true, false>(CL, q, joy, B, x0, S, obsn, c);
+      A1_CLOCK(64, 22);
+      ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+      A1_CLOCK(64, 23);
+#endif
       lds_barrier();
 #pragma unroll
       for (int f = 0; f < F0; ++f) xpre[f] = *reinterpret_cast<const float4 *>(x0 + 64 * f + 4 * s);
@@ -1584,8 +1620,9 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
 #pragma unroll
         for (int f = 0; f < HF; ++f) {
           const float4 x = *reinterpret_cast<const float4 *>(xr + 64 * f);
-          acc = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{wo[f].x, wo[f].y}, acc);
-          acc = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{wo[f].z, wo[f].w}, acc);
+          const float4 wv = W0L ? wol[f * 256 + c] : wo[f];
+          acc = __builtin_elementwise_fma(f32x2{x.x, x.y}, f32x2{wv.x, wv.y}, acc);
+          acc = __builtin_elementwise_fma(f32x2{x.z, x.w}, f32x2{wv.z, wv.w}, acc);
         }
         float p[1] = {acc.x + acc.y};
         const float v = a1_reduce<1>(p);
@@ -1608,16 +1645,27 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
     }
     A1_STAMP(64, 8);
     A1_CLOCK(64, 14);
-    if constexpr (CTL) {  // the NaN flags, every output drained, then the done word
+    if constexpr (CTL) {  // the new observation rows and NaN flags, every output drained, then the done word
+      for (int i = c; i < B * in_dim; i += 64 * CW) {
+        int ii = i;
+        asm volatile("" : "+v"(ii));  // (the address formed here, not hoisted and spilled)
+        C.obs[ii] = obsn[ii];
+      }
       if ((word & GO2PI_RES_STATUS) && c < B) {
         int cs = c;
         asm volatile("" : "+v"(cs));  // (the address formed here, not hoisted and spilled)
         C.status[cs] = CL.nanf[cs];
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores are in the L2
       lds_barrier();
       if (c < GO2PI_TILE_ROWS) CL.nanf[c] = 0u;  // (read above, before the barrier)
-      if (c == 0) __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (c == 0) {
+        // the plain stores of the outputs (host staging) written back from the L2 before the
+        // done word (a system-scope release: one L2 write-back for the whole workgroup's
+        // stores; without it the host read stale staging behind a valid done word)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       A1_STAMP(64, 9);
     }
     ++nreq;
@@ -1721,10 +1769,12 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
   // sweeps in flight, 1 / 2 / 4)
   const A1Shape a1 = act1_shape(p);
   if (a1.nl && !std::getenv("GO2PI_RES_R1W")) {
-    // (the controller form: the assembly's image and layer 0's weights, lane-major, besides)
+    // (the controller form: the assembly's image, layer 0's weights, lane-major, and the
+    // new observation rows besides)
     const size_t lds1 = sizeof(float) * (3 * (size_t)GO2PI_SMALL_MAXB * p.lds_stride + 4 +
                                          (ctl ? (size_t)ctl_lds_floats(GO2PI_SMALL_MAXB, p.in_dim) +
-                                                    (size_t)a1.f0 * (a1.h / 32) * 512 * 4
+                                                    (size_t)a1.f0 * (a1.h / 32) * 512 * 4 + (size_t)(a1.h / 64) * 256 * 4 +
+                                                    (size_t)GO2PI_SMALL_MAXB * p.in_dim
                                               : 0));
     auto go1 = [&](auto kern, int cw) {
       if (lds1 > 64 * 1024) {

@@ -105,26 +105,32 @@ def one_workgroup(args, st, ts, np):
     layers), 8 the answer's granule stores issued (wave 1's head output)."""
     rows = st[(st[:, 0] > 0) & (st[:, 8] > 0)]
     rel = (rows - rows[:, 0:1]) * 10.0 / 1e3
-    names = {1: "input staged", 8: "answer issued", 9: "done word (controller form)"}
+    names = {1: "input staged", 8: "answer issued", 9: "done word (controller form)",
+             10: "request staged (controller form: before the assembly)"}
     for l in range(6):
         names[2 + l] = f"layer{l} done"
-    med, prev = {}, 0.0
-    for s_ in sorted(names):
+    med, prev, at = {}, 0.0, {}
+    for s_ in names:
         ok = rows[:, s_] > 0
-        if ok.sum() < len(rows) // 2:
-            continue
-        m = float(np.median(rel[ok, s_]))
-        med[names[s_]] = {"at_us": round(m, 3), "step_us": round(m - prev, 3)}
-        prev = m
+        if ok.sum() >= len(rows) // 2:
+            at[s_] = float(np.median(rel[ok, s_]))
+    for s_ in sorted(at, key=lambda k: at[k]):  # in time order
+        med[names[s_]] = {"at_us": round(at[s_], 3), "step_us": round(at[s_] - prev, 3)}
+        prev = at[s_]
     gaps = (rows[1:, 0] - rows[:-1, 8]) * 10.0 / 1e3
     # shader clock (s_memtime, slots 13..30) over the wall clock from seen (15) to answer (14)
     dwall = (rows[:, 8] - rows[:, 0]) * 10e-9
     ghz = (rows[:, 14] - rows[:, 15]) / np.maximum(dwall, 1e-9) / 1e9
     cyc = {}
-    marks = [(13, "input staged")]
+    marks = [(11, "request staged (controller form)"), (19, "controller parameters loaded"),
+             (20, "appended values stored"), (21, "shifted values stored"), (22, "appended again (GO2PI_DIAG_ASM2)"),
+             (23, "shifted again (GO2PI_DIAG_ASM2)"), (13, "input staged")]
+    act1_ctl = (rows[:, 11] > 0).sum() >= len(rows) // 2  # (its slots 19-21 are the assembly's)
     for l in range(3):
-        marks += [(16 + 3 * l, f"layer{l} fma done"), (17 + 3 * l, f"layer{l} group sums done"),
-                  (18 + 3 * l, f"layer{l} outputs stored"), (25 + l, f"layer{l} barrier passed")]
+        if l == 0 or not act1_ctl:
+            marks += [(16 + 3 * l, f"layer{l} fma done"), (17 + 3 * l, f"layer{l} group sums done"),
+                      (18 + 3 * l, f"layer{l} outputs stored")]
+        marks += [(25 + l, f"layer{l} barrier passed")]
     marks += [(14, "answer issued")]
     prev = rows[:, 15]
     for s_, nm in marks:
