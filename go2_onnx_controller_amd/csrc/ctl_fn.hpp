@@ -441,6 +441,40 @@ __device__ __forceinline__ void ctl_store(const CtlView V, int row, int n, float
   if (V.kd) V.kd[o] = V.kd_run;
 }
 
+// The resident controller form's answer (policy_act1_kernel, CTL): each output value as
+// an {epoch, 32 bits} granule at its ctl_gran offset, stored at system scope (written
+// through to the host's pinned memory on its own); the host checks every tag, so no
+// drain, fence or done word follows the last store. V's output pointers only say which
+// outputs the call asked for. Per element the operations of ctl_store. The caller's
+// consecutive threads take consecutive (row, joint) outputs: every store instruction
+// then writes one contiguous range.
+__device__ __forceinline__ void gran_put(unsigned long long *g, unsigned e, unsigned bits) {
+  __hip_atomic_store(g, ((unsigned long long)e << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// two consecutive granules {lo, e}, {hi, e} in one 16-byte system-scope store (each
+// granule checked on its own: a torn 16-byte write is harmless)
+__device__ __forceinline__ void gran_put2(unsigned long long *g, unsigned e, unsigned lo, unsigned hi) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {lo, e, hi, e};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(g), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ctl_store_gran(const CtlView V, int row, int n, float v, unsigned long long *g,
+                                               const CtlGran G, unsigned e) {
+#pragma clang fp contract(off)
+  float a = v < -V.lim ? -V.lim : (V.lim < v ? V.lim : v);
+  const bool stop = V.jy && V.jy[(row - V.row0) * GO2PI_CTL_JOY_DIM + 4] != 0.f;
+  a *= stop ? 0.f : 1.f;
+  const int o = row * GO2PI_CTL_DOF + n;
+  gran_put(g + G.act + o, e, __float_as_uint(a));
+  auto put64 = [&](int off, double x) {  // both halves' granules in one 16-byte store
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    gran_put2(g + off + 2 * o, e, (unsigned)b, (unsigned)(b >> 32));
+  };
+  if (V.q_des) put64(G.qdes, V.q0[n] + (double)a * V.scale);
+  if (V.kp) put64(G.kp, stop ? V.kp_stop : V.kp_run);
+  if (V.kd) put64(G.kd, V.kd_run);
+}
+
 // The same for joints n .. n + 3 of one robot (n % 4 == 0, all four < 12): the
 // joystick row read once, and every output as 16-byte stores (the batched kernel's
 // head lane holds four consecutive joints). Per element the operations of ctl_store.

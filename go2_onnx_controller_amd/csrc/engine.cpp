@@ -189,6 +189,7 @@ struct go2pi_engine {
   float *h_obs = nullptr, *h_act = nullptr;  // pinned, host-mapped
   float *m_obs = nullptr, *m_act = nullptr;  // device aliases of the above
   unsigned long long *h_actg = nullptr, *m_actg = nullptr;  // resident act(): {epoch, value} action granules
+  size_t n_actg = 0;
   hipGraphExec_t graphs[GO2PI_SMALL_MAXB + 1] = {};
   hipGraph_t graph_defs[GO2PI_SMALL_MAXB + 1] = {};
   go2pi_cost cost{};
@@ -211,6 +212,7 @@ struct go2pi_engine {
   bool resident_ctl = false;  // the live kernel is the controller-tick form
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
+  bool ctl_gran_ok = false;   // ... answered in granules (policy_act1_kernel, r05): no done word per tick
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // request granules: host view, device view
   size_t req_bar_bytes = 0;  // > 0: the ring is in device memory the host writes through the BAR (bar_take)
@@ -331,7 +333,7 @@ struct go2pi_engine {
                 "hipMemsetAsync");
     __atomic_store_n(h_req, 0ull, __ATOMIC_SEQ_CST);
     __atomic_store_n(h_done, 0u, __ATOMIC_SEQ_CST);
-    std::memset(h_actg, 0, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)model.out_dim);
+    std::memset(h_actg, 0, sizeof(unsigned long long) * n_actg);
     if (ctl ? resident1_ctl : resident1)
       hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, ctl,
                                         stream),
@@ -374,6 +376,77 @@ struct go2pi_engine {
            __atomic_load_n(h_done, __ATOMIC_ACQUIRE) != GO2PI_RES_LEAVE &&
            epoch <= 0xFFFFFFF0u - 2 * ((unsigned)prog.nl + 2);
   }
+  // The granules of one request's answer: {offset, count} ranges of h_actg (act(): the
+  // action rows; the controller form's: the requested outputs, the observation rows
+  // first, as the kernel stores them first). The scan resumes where it stopped.
+  struct GranScan {
+    int r[6][2];
+    int nr = 0, ri = 0, k = 0;
+    void add(int off, int n) {
+      r[nr][0] = off;
+      r[nr++][1] = n;
+    }
+  };
+  GranScan gran_scan(bool ctl, int64_t batch, unsigned flags) const {
+    GranScan sc;
+    const int b = (int)batch;
+    if (!ctl) {
+      sc.add(0, b * model.out_dim);
+      return sc;
+    }
+    const go2pi::CtlGran G = go2pi::ctl_gran(model.in_dim);
+    sc.add(G.obs, b * model.in_dim);
+    if (flags & GO2PI_RES_STATUS) sc.add(G.status, b);
+    sc.add(G.act, b * GO2PI_CTL_DOF);
+    if (flags & GO2PI_RES_QDES) sc.add(G.qdes, 2 * b * GO2PI_CTL_DOF);
+    if (flags & GO2PI_RES_KP) sc.add(G.kp, 2 * b * GO2PI_CTL_DOF);
+    if (flags & GO2PI_RES_KD) sc.add(G.kd, 2 * b * GO2PI_CTL_DOF);
+    return sc;
+  }
+  // true once every granule of sc carries tag e0
+  bool gran_done(GranScan &sc, unsigned e0) const {
+    for (; sc.ri < sc.nr; ++sc.ri, sc.k = 0) {
+      const unsigned long long *g = h_actg + sc.r[sc.ri][0];
+      const int n = sc.r[sc.ri][1];
+      while (sc.k < n && (unsigned)(__atomic_load_n(g + sc.k, __ATOMIC_ACQUIRE) >> 32) == e0) ++sc.k;
+      if (sc.k < n) return false;
+    }
+    return true;
+  }
+  // the act() answer's values to h_act
+  void act_take(int64_t batch) {
+    const int nout = (int)batch * model.out_dim;
+    for (int j = 0; j < nout; ++j) {
+      const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
+      std::memcpy(h_act + j, &bits, 4);
+    }
+  }
+  // the controller form's answer granules to the caller's buffers (ctl_gran_ok)
+  void ctl_take(int64_t batch, float *obs, float *action, double *q_des, double *kp, double *kd,
+                uint32_t *status) const {
+    const go2pi::CtlGran G = go2pi::ctl_gran(model.in_dim);
+    const int b = (int)batch, nd = b * GO2PI_CTL_DOF;
+    auto lo = [&](int i) { return (uint32_t)__atomic_load_n(h_actg + i, __ATOMIC_RELAXED); };
+    auto f64 = [&](int off, double *dst) {
+      for (int i = 0; i < nd; ++i) {
+        const uint64_t bits = (uint64_t)lo(off + 2 * i) | ((uint64_t)lo(off + 2 * i + 1) << 32);
+        std::memcpy(dst + i, &bits, 8);
+      }
+    };
+    for (int i = 0; i < b * model.in_dim; ++i) {
+      const uint32_t bits = lo(G.obs + i);
+      std::memcpy(obs + i, &bits, 4);
+    }
+    for (int i = 0; i < nd; ++i) {
+      const uint32_t bits = lo(G.act + i);
+      std::memcpy(action + i, &bits, 4);
+    }
+    if (q_des) f64(G.qdes, q_des);
+    if (kp) f64(G.kp, kp);
+    if (kd) f64(G.kd, kd);
+    if (status)
+      for (int i = 0; i < b; ++i) status[i] = lo(G.status + i);
+  }
   bool resident_serve(const go2pi::DevCtl *ctl, const float *rows, int64_t batch, unsigned flags) {
     if (resident_live && resident_ctl != (ctl != nullptr)) {  // the other form is live
       need_device();
@@ -411,45 +484,37 @@ struct go2pi_engine {
       if (req_bar_bytes) _mm_sfence();  // the BAR mapping is write-combined: send the request now
       const auto t0 = std::chrono::steady_clock::now();
       unsigned d;
-      if (ctl) {  // the controller form: a done word behind the drained outputs
+      // act() and the granule controller form: the answer granules themselves, every tag =
+      // this request's epoch; the r04 / multi-workgroup controller forms: a done word
+      // behind the drained outputs
+      const bool gran = !ctl || ctl_gran_ok;
+      if (!gran) {
         for (unsigned it = 0; (d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) != e0 && d != GO2PI_RES_LEAVE; ++it) {
           __builtin_ia32_pause();
           if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
         }
-      } else {  // act(): the action granules themselves, every tag = this request's epoch
-        const int nout = (int)batch * model.out_dim;
+      } else {
+        GranScan sc = gran_scan(ctl != nullptr, batch, flags);
         for (unsigned it = 0;; ++it) {
-          int i = 0;
-          while (i < nout && (unsigned)(__atomic_load_n(h_actg + i, __ATOMIC_RELAXED) >> 32) == e0) ++i;
-          if (i == nout) {
+          if (gran_done(sc, e0)) {
             d = e0;
-            for (int j = 0; j < nout; ++j) {
-              const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
-              std::memcpy(h_act + j, &bits, 4);
-            }
             break;
           }
           if ((d = __atomic_load_n(h_done, __ATOMIC_ACQUIRE)) == GO2PI_RES_LEAVE) {
             // the kernel may have answered this request and then left (a LEAVE header
-            // from evict_residents, or a moved yield counter): its action granules are
+            // from evict_residents, or a moved yield counter): its answer granules are
             // acknowledged before the LEAVE done word (resident.hip: vmcnt(0), barrier,
             // then done), so a rescan after seeing LEAVE finds them if it served the
             // request. Treating a served request as unserved would run it twice: for a
             // GRU / LSTM policy, advancing the hidden state twice.
-            int k = 0;
-            while (k < nout && (unsigned)(__atomic_load_n(h_actg + k, __ATOMIC_ACQUIRE) >> 32) == e0) ++k;
-            if (k == nout) {
-              d = e0;
-              for (int j = 0; j < nout; ++j) {
-                const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
-                std::memcpy(h_act + j, &bits, 4);
-              }
-            }
+            GranScan again = gran_scan(ctl != nullptr, batch, flags);
+            if (gran_done(again, e0)) d = e0;
             break;
           }
           __builtin_ia32_pause();
           if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
         }
+        if (d == e0 && !ctl) act_take(batch);
       }
       res_last = std::chrono::steady_clock::now();
       if (d == e0) return true;
@@ -458,15 +523,10 @@ struct go2pi_engine {
       // (h_err set) is a device-side protocol fault and is reported, not retried
       need_device();
       resident_stop();
-      if (!ctl) {  // the kernel has exited (stream synced): a request it served has every granule
-        const int nout = (int)batch * model.out_dim;
-        int k = 0;
-        while (k < nout && (unsigned)(__atomic_load_n(h_actg + k, __ATOMIC_ACQUIRE) >> 32) == e0) ++k;
-        if (k == nout) {
-          for (int j = 0; j < nout; ++j) {
-            const unsigned bits = (unsigned)__atomic_load_n(h_actg + j, __ATOMIC_RELAXED);
-            std::memcpy(h_act + j, &bits, 4);
-          }
+      if (gran) {  // the kernel has exited (stream synced): a request it served has every granule
+        GranScan again = gran_scan(ctl != nullptr, batch, flags);
+        if (gran_done(again, e0)) {
+          if (!ctl) act_take(batch);
           return true;
         }
       }
@@ -917,7 +977,9 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       } else {
         e.palloc(&e.h_req, &e.m_req, sizeof(unsigned long long) * nreq);
       }
-      e.palloc(&e.h_actg, &e.m_actg, sizeof(unsigned long long) * GO2PI_SMALL_MAXB * (size_t)m.out_dim);
+      // (the controller form's answer granules too: ctl_gran)
+      e.n_actg = std::max((size_t)GO2PI_SMALL_MAXB * m.out_dim, (size_t)go2pi::ctl_gran(m.in_dim).total);
+      e.palloc(&e.h_actg, &e.m_actg, sizeof(unsigned long long) * e.n_actg);
       e.d_mirror = e.dalloc<unsigned long long>(1 + GO2PI_SMALL_MAXB * (size_t)m.in_dim);
       int khz = 0;
       hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.device), "hipDeviceGetAttribute");
@@ -990,6 +1052,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   // the multi-workgroup form, A/B diagnostics)
   e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, false) && !std::getenv("GO2PI_RES_MULTI");
   e.resident1_ctl = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, true) && !std::getenv("GO2PI_RES_MULTI");
+  e.ctl_gran_ok = e.resident1_ctl && go2pi::resident1_ctl_granules(p);
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
@@ -1418,6 +1481,10 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
         std::memcpy(rows + batch * (GO2PI_CTL_STATE_DIM + GO2PI_CTL_JOY_DIM + in_dim), action, n_act);
         if (!e->resident_serve(&all, rows, batch, flags)) return 1;
         e->check_handoff();
+        if (e->ctl_gran_ok) {
+          e->ctl_take(batch, obs, action, q_des, kp, kd, status);
+          return GO2PI_OK;
+        }
         std::memcpy(obs, e->h_ctl + L.obs, n_obs);
         std::memcpy(action, e->h_ctl + L.action, n_act);
         if (q_des) std::memcpy(q_des, e->h_ctl + L.q_des, n_d);
@@ -1503,12 +1570,16 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
       const bool synced = served || (single && e->spin_done());
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
       e->check_handoff();
-      std::memcpy(obs, e->h_ctl + L.obs, n_obs);
-      std::memcpy(action, e->h_ctl + L.action, n_act);
-      if (q_des) std::memcpy(q_des, e->h_ctl + L.q_des, n_d);
-      if (kp) std::memcpy(kp, e->h_ctl + L.kp, n_d);
-      if (kd) std::memcpy(kd, e->h_ctl + L.kd, n_d);
-      if (status) std::memcpy(status, e->h_ctl + L.status, n_st);
+      if (served && e->ctl_gran_ok) {
+        e->ctl_take(batch, obs, action, q_des, kp, kd, status);
+      } else {
+        std::memcpy(obs, e->h_ctl + L.obs, n_obs);
+        std::memcpy(action, e->h_ctl + L.action, n_act);
+        if (q_des) std::memcpy(q_des, e->h_ctl + L.q_des, n_d);
+        if (kp) std::memcpy(kp, e->h_ctl + L.kp, n_d);
+        if (kd) std::memcpy(kd, e->h_ctl + L.kd, n_d);
+        if (status) std::memcpy(status, e->h_ctl + L.status, n_st);
+      }
     } else {
       auto d2h = [&](void *dst, size_t off, size_t n) {
         hip_check(hipMemcpyAsync(dst, dev + off, n, hipMemcpyDeviceToHost, e->stream), "hipMemcpyAsync D2H");

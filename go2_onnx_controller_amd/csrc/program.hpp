@@ -231,6 +231,21 @@ int launch_resident(const DevProgram &p, const DevProgram *p_dev, const unsigned
 // dense policies of <= 4 layers whose weights fit one CU's registers, at most 16
 // outputs. Same request / answer / leave protocol as launch_resident.
 bool resident1_fits(const DevProgram &p, bool ctl);  // ctl: the controller form (512 threads)
+// The controller form answers in granules too when policy_act1_kernel serves it (r05;
+// true here): actg holds ctl_gran(in_dim).total granules, each output value tagged with
+// the request's epoch, and there is no done word per request (the r04 forms and
+// launch_resident's drain the plain outputs into ctl's staging, then set done).
+bool resident1_ctl_granules(const DevProgram &p);
+// Offsets (in granules) of the controller form's answer, fixed for GO2PI_SMALL_MAXB rows:
+// action [8][12], q_des / kp / kd [8][12][2] (each double's low then high 32 bits),
+// the new observation rows [8][in_dim], status [8]. Only the requested outputs are written.
+struct CtlGran {
+  int act, qdes, kp, kd, obs, status, total;
+};
+constexpr CtlGran ctl_gran(int in_dim) {  // (constexpr: callable from device code too)
+  constexpr int R = GO2PI_SMALL_MAXB, D = GO2PI_CTL_DOF;
+  return CtlGran{0, R * D, 3 * R * D, 5 * R * D, 7 * R * D, 7 * R * D + R * in_dim, 7 * R * D + R * in_dim + R};
+}
 // ctl non-null: the controller-tick form (launch_resident's ctl semantics).
 int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,

@@ -864,6 +864,8 @@ bool resident1_fits(const DevProgram &p, bool ctl) {
   return p.L[0].K_pad <= nt;
 }
 
+bool resident1_ctl_granules(const DevProgram &p) { return act1_shape(p).nl && !std::getenv("GO2PI_RES_R1W"); }
+
 // CTL: the controller tick (go2pi_controller_step at batch <= 8), as the multi-
 // workgroup kernel's controller form: the request carries the tick's raw rows
 // (state | joystick | previous obs | previous action, as tagged granules), the
@@ -1514,7 +1516,6 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       ++nreq;
       continue;
     }
-    CtlView cv{};
     if constexpr (CTL) {
       A1_STAMP(64, 10);
       // the observation assembled from the image: the new rows to LDS (obsn; they go to the
@@ -1533,25 +1534,40 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       // (x0's padding columns stay zero from the start and its rows past B are never read:
       // the shift pass leaves them alone)
       static_assert(CW >= 7, "the controller form's assembly runs one history block per compute wave");
+      // the shift pass starts on the last compute wave, the one without a block (at batch 1
+      // its elements all fit that wave: the two passes run side by side)
+      const int cr = c + 64 < 64 * CW ? c + 64 : c + 64 - 64 * CW;
       if (q.pro.sub || q.pro.div || q.pro.mul) {
         ctl_append_waves<true, true>(CL, q, joy, B, x0, S, obsn, c);
         A1_CLOCK(64, 20);
-        ctl_shift<true, true, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+        ctl_shift<true, true, 2, false>(CL, q, B, x0, S, obsn, cr, 64 * CW);
       } else {
         ctl_append_waves<true, false>(CL, q, joy, B, x0, S, obsn, c);
         A1_CLOCK(64, 20);
-        ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+        ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, cr, 64 * CW);
       }
       A1_CLOCK(64, 21);
 #ifdef GO2PI_DIAG_ASM2  // both passes again, warm (instruction fetch and first touches vs. work): slots 22-23
       ctl_append_waves<true, false>(CL, q, joy, B, x0, S, obsn, c);
       A1_CLOCK(64, 22);
-      ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, c, 64 * CW);
+      ctl_shift<true, false, 2, false>(CL, q, B, x0, S, obsn, cr, 64 * CW);
       A1_CLOCK(64, 23);
 #endif
       lds_barrier();
 #pragma unroll
       for (int f = 0; f < F0; ++f) xpre[f] = *reinterpret_cast<const float4 *>(x0 + 64 * f + 4 * s);
+      // the new observation rows and NaN flags answer now, their stores overlapping the layers
+      const CtlGran G = ctl_gran(in_dim);
+      for (int i = c; i < B * in_dim; i += 64 * CW) {
+        int ii = i;
+        asm volatile("" : "+v"(ii));  // (the addresses formed here, not hoisted and spilled)
+        gran_put(actg + G.obs + ii, e, __float_as_uint(obsn[ii]));
+      }
+      if ((word & GO2PI_RES_STATUS) && c < B) {
+        int cs = c;
+        asm volatile("" : "+v"(cs));
+        gran_put(actg + G.status + cs, e, CL.nanf[cs]);
+      }
     }
     A1_STAMP(64, 1);
     A1_CLOCK(64, 13);
@@ -1604,14 +1620,6 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
       Y = Y == xa ? xb : xa;
     }
     // ---- the head: 16 outputs, one per DPP row of compute waves 0..3
-    if constexpr (CTL) {  // (the outputs' view formed here: live across the layers, its fields spilled)
-      DevCtl cc = C;
-      if (!(word & GO2PI_RES_JOY)) cc.joy = nullptr;
-      if (!(word & GO2PI_RES_QDES)) cc.q_des = nullptr;
-      if (!(word & GO2PI_RES_KP)) cc.kp = nullptr;
-      if (!(word & GO2PI_RES_KD)) cc.kd = nullptr;
-      cv = ctl_view(cc, CL, 0);
-    }
     if (c < 256) {
       const int A = AS != 0xFFFFFFFFu ? (int)((AS >> (4 * (NL - 1))) & 15u) : lact[NL - 1];
       for (int b = 0; b < B; ++b) {
@@ -1631,9 +1639,7 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
           if (post_tanh) y = tanhf(y);
           y = clip_nan(y, clo, chi) * pscale;
           if constexpr (CTL) {
-            int n = grp;
-            asm volatile("" : "+v"(n));  // (per-lane output addresses formed here, not hoisted and spilled)
-            ctl_store(cv, b, n, y);
+            Y[b * 16 + grp] = y;  // (the answer granules from there: below)
           } else {
             int n = grp;
             asm volatile("" : "+v"(n));  // (the granule address formed here, not hoisted and spilled)
@@ -1645,26 +1651,26 @@ __global__ __launch_bounds__(a1_nt(CW)) void policy_act1_kernel(const DevProgram
     }
     A1_STAMP(64, 8);
     A1_CLOCK(64, 14);
-    if constexpr (CTL) {  // the new observation rows and NaN flags, every output drained, then the done word
-      for (int i = c; i < B * in_dim; i += 64 * CW) {
-        int ii = i;
-        asm volatile("" : "+v"(ii));  // (the address formed here, not hoisted and spilled)
-        C.obs[ii] = obsn[ii];
-      }
-      if ((word & GO2PI_RES_STATUS) && c < B) {
-        int cs = c;
-        asm volatile("" : "+v"(cs));  // (the address formed here, not hoisted and spilled)
-        C.status[cs] = CL.nanf[cs];
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores are in the L2
+    if constexpr (CTL) {
+      // The answer's action, q_des, kp and kd granules, written by consecutive threads from
+      // the head's outputs gathered in LDS (Y: not the head's input), so that each store
+      // instruction covers one contiguous range of the host's staging: stored by the head's
+      // lanes themselves (four per wave, each output's granules apart) the partial-line
+      // PCIe writes cost ~6 us per tick. The image's joystick and q0 rows stay valid: the
+      // polling wave stages the next request only after the host has read this answer.
       lds_barrier();
-      if (c < GO2PI_TILE_ROWS) CL.nanf[c] = 0u;  // (read above, before the barrier)
-      if (c == 0) {
-        // the plain stores of the outputs (host staging) written back from the L2 before the
-        // done word (a system-scope release: one L2 write-back for the whole workgroup's
-        // stores; without it the host read stale staging behind a valid done word)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (c < GO2PI_TILE_ROWS) CL.nanf[c] = 0u;  // (the status granule read it after the assembly)
+      if (c < B * GO2PI_CTL_DOF) {
+        DevCtl cc = C;
+        if (!(word & GO2PI_RES_JOY)) cc.joy = nullptr;
+        if (!(word & GO2PI_RES_QDES)) cc.q_des = nullptr;
+        if (!(word & GO2PI_RES_KP)) cc.kp = nullptr;
+        if (!(word & GO2PI_RES_KD)) cc.kd = nullptr;
+        const CtlView cv = ctl_view(cc, CL, 0);
+        int i = c;
+        asm volatile("" : "+v"(i));  // (the addresses formed here, not hoisted and spilled)
+        const int b = i / GO2PI_CTL_DOF, n = i - b * GO2PI_CTL_DOF;
+        ctl_store_gran(cv, b, n, Y[b * 16 + n], actg, ctl_gran(in_dim), e);
       }
       A1_STAMP(64, 9);
     }

@@ -5,7 +5,8 @@
  * kp / kd and the NaN status out. The resident kernel serves it (resident_ms = 100;
  * argv[4] = 0: one launch per tick). Timed per call with CLOCK_MONOTONIC over <warm>
  * untimed then <iters> timed ticks; prints p50 / p99 in microseconds.
- * Usage: ctl_lat <model.onnx> <iters> <warm> [resident_ms] */
+ * Usage: ctl_lat <model.onnx> <iters> <warm> [resident_ms] [min]
+ * ("min": q_des / kp / kd / status not asked for, only the observation and the action) */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -22,6 +23,7 @@ static int cmp_d(const void *a, const void *b) {
 int main(int argc, char **argv) {
   if (argc < 4) return 2;
   const int iters = atoi(argv[2]), warm = atoi(argv[3]);
+  const int lean = argc > 5 && strcmp(argv[5], "min") == 0;
   go2pi_opts o;
   go2pi_default_opts(&o);
   o.max_batch = 8;
@@ -43,7 +45,8 @@ int main(int argc, char **argv) {
     state[7 + t % 12] += 0.001f; /* the joints move every tick */
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
-    const int rc = go2pi_controller_step(e, state, joy, obs, action, q_des, kp, kd, &status, 1);
+    const int rc = lean ? go2pi_controller_step(e, state, joy, obs, action, NULL, NULL, NULL, NULL, 1)
+                        : go2pi_controller_step(e, state, joy, obs, action, q_des, kp, kd, &status, 1);
     clock_gettime(CLOCK_MONOTONIC, &b);
     if (rc) {
       printf("controller_step: %s\n", go2pi_last_error());

@@ -14,6 +14,7 @@ L=$R/go2_onnx_controller_amd/lib
 g++ -std=c++20 -O2 -I$R/include $R/tests/cpp/controller_shape.cpp -L$L -lonnx_actor -Wl,-rpath,$L -o $R/build/controller_shape || exit 1
 M=$R/tests/golden/model.onnx
 for round in 1 2 3; do
+  [ -n "$SKIP_ACT" ] && break
   for v in ${VARIANTS:-c8d2 c8d1 c8d2host c4d2 r1w launch}; do
     case $v in
       c8d2host) env="GO2PI_A1_CW=8 GO2PI_REQ_HOST=1" ;;
@@ -33,12 +34,14 @@ gcc -O2 -I$R/include $R/tests/cpp/ctl_lat.c -L$L -lgo2pi -Wl,-rpath,$L -o $R/bui
 for round in 1 2; do
   for v in ${CTL_VARIANTS:-a1 a1host r1w launch}; do
     case $v in
-      a1) env=""; rm=100 ;;
-      a1host) env="GO2PI_REQ_HOST=1"; rm=100 ;;
-      r1w) env="GO2PI_RES_R1W=1"; rm=100 ;;
-      launch) env=""; rm=0 ;;
+      a1) env=""; rm=100; x="" ;;
+      a1min) env=""; rm=100; x=min ;;  # (only obs and action asked for)
+      a1host) env="GO2PI_REQ_HOST=1"; rm=100; x="" ;;
+      r1w) env="GO2PI_RES_R1W=1"; rm=100; x="" ;;
+      r1wmin) env="GO2PI_RES_R1W=1"; rm=100; x=min ;;
+      launch) env=""; rm=0; x="" ;;
     esac
-    r=$(env $env timeout -k 10 60 $R/build/ctl_lat $M 10000 1000 $rm) || { echo "ctl_lat $v failed: $r"; exit 1; }
+    r=$(env $env timeout -k 10 60 $R/build/ctl_lat $M 10000 1000 $rm $x) || { echo "ctl_lat $v failed: $r"; exit 1; }
     echo "ctl round $round $v $(echo $r | tr '\n' ' ')" | tee -a $O/ab.txt
   done
 done
