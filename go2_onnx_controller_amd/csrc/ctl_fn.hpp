@@ -23,25 +23,35 @@ namespace go2pi {
 // the (x,y,z,w) coefficients), and q * v = _transformVector:
 // uv = 2 (q.vec × v), r = (v + w uv) + q.vec × uv. Every operation rounds to
 // fp32 in that order (no fma contraction), like the reference's x86 build.
-__device__ __forceinline__ float ctl_gravity(const float *st, float v0, float v1, float v2, int i) {
+// Four lanes of a quad per robot: lane i of the quad divides one
+// quaternion coefficient (i = 0: w, 1: -x, 2: -y, 3: -z, over the same n2) and takes
+// the other three quotients from its neighbours (DPP quad broadcasts), then forms
+// component i (< 3) branch-free: one IEEE division per lane instead of four (the
+// batch-1 resident kernel's assembly waits for this block: ~1.4K cycles with all four
+// divisions and a branch per component in every lane). All four lanes of the quad active.
+__device__ __forceinline__ float quad_bcast(float v, int k) {
+  const int b = __float_as_int(v);
+  switch (k) {  // quad_perm [k, k, k, k]
+    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0xFF, 0xF, 0xF, false));
+  }
+}
+__device__ __forceinline__ float ctl_gravity_quad(const float *st, float v0, float v1, float v2, int i) {
 #pragma clang fp contract(off)
   const float w = st[0], x = st[1], y = st[2], z = st[3];
   const float n2 = (x * x + z * z) + (y * y + w * w);
-  float qw = 0.f, qx = 0.f, qy = 0.f, qz = 0.f;
-  if (n2 > 0.f) {
-    qx = -x / n2;
-    qy = -y / n2;
-    qz = -z / n2;
-    qw = w / n2;
-  }
+  const float num = i == 0 ? w : (i == 1 ? -x : (i == 2 ? -y : -z));
+  const float qi = n2 > 0.f ? num / n2 : 0.f;
+  const float qw = quad_bcast(qi, 0), qx = quad_bcast(qi, 1), qy = quad_bcast(qi, 2), qz = quad_bcast(qi, 3);
   float u0 = qy * v2 - qz * v1, u1 = qz * v0 - qx * v2, u2 = qx * v1 - qy * v0;
   u0 += u0;
   u1 += u1;
   u2 += u2;
   const float c0 = qy * u2 - qz * u1, c1 = qz * u0 - qx * u2, c2 = qx * u1 - qy * u0;
-  if (i == 0) return (v0 + qw * u0) + c0;
-  if (i == 1) return (v1 + qw * u1) + c1;
-  return (v2 + qw * u2) + c2;
+  const float r0 = (v0 + qw * u0) + c0, r1 = (v1 + qw * u1) + c1, r2 = (v2 + qw * u2) + c2;
+  return i == 0 ? r0 : (i == 1 ? r1 : r2);
 }
 
 // Direct-to-LDS copy of n contiguous floats (global_load_lds_dword: no VGPR
@@ -49,6 +59,7 @@ __device__ __forceinline__ float ctl_gravity(const float *st, float v0, float v1
 // for ceil64(n) floats (the tail lanes re-read element n-1). Complete after
 // the next __syncthreads() (its fence waits vmcnt(0)).
 typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;  // (a global, not flat, access)
 typedef __attribute__((address_space(3))) void lvoid_t;
 // Before the barrier that hands LDS-DMA'd bytes to OTHER waves, each issuing wave
 // waits for its own direct-to-LDS loads: the compiler's barrier fence does not
@@ -191,13 +202,27 @@ __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, 
   const int k0 = H * cum + (H - 1) * d;  // the block's first appended column
   int t = tid - (64 * BK) % nt;
   if (t < 0) t += nt;
+  if constexpr (BK == 0) {  // gravity: a quad of lanes per robot (ctl_gravity_quad; nt % 4 == 0)
+    for (int e = t; e < nrows * 4; e += nt) {
+      const int r = e >> 2, c = e & 3, k = k0 + c;
+#if defined(GO2PI_DIAG_GRAV_TRIVIAL)  // (diagnostics: the block's cost without its arithmetic)
+      const float x = st_l[r * GO2PI_CTL_STATE_DIM + c];
+#else
+      const float x = ctl_gravity_quad(st_l + r * GO2PI_CTL_STATE_DIM, q.g0, q.g1, q.g2, c);
+#endif
+      if (c < 3) {
+        nanm |= (__builtin_isnan(x) ? 1u : 0u) << r;
+        if constexpr (TILE) raw[r * in_dim + k] = x;
+        dst[r * ds + k] = ctl_pro<TILE, ARITH>(q, x, k);
+      }
+    }
+    return;
+  }
   for (int e = t; e < nrows * d; e += nt) {
     const int r = e / d, c = e - r * d, k = k0 + c;
     const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
     float x;
-    if constexpr (BK == 0) {
-      x = ctl_gravity(st, q.g0, q.g1, q.g2, c);
-    } else if constexpr (BK == 1) {
+    if constexpr (BK == 1) {
       x = st[4 + c];  // imu gyroscope (controller.hpp:105-109)
     } else if constexpr (BK == 2) {
       // vel_cmd from the joystick (controller.cpp:173-179); kept (the previous
@@ -269,7 +294,9 @@ __device__ __forceinline__ void ctl_append_waves(const CtlLds L, const CtlQ &q, 
   unsigned nanm = 0u;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   switch (w) {
+#ifndef GO2PI_DIAG_NO_BLOCK0
     case 0: ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
+#endif
     case 1: ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
     case 2: ctl_append_block<2, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;
     case 3: ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, lane, 64, nanm); break;

@@ -35,13 +35,15 @@
 #ifdef GO2PI_DIAG_CLOCK
 #define GO2PI_STAMP_AT(row, cond, slot)                                  \
   do {                                                                   \
-    if ((row) && (cond)) (row)[slot] = __builtin_amdgcn_s_memtime();     \
+    if ((row) && (cond)) ((__attribute__((address_space(1))) unsigned long long *)(row))[slot] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #define GO2PI_STAMP(P, cond, slot) \
   GO2PI_STAMP_AT((P).stamps ? (P).stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, cond, slot)
 #define GO2PI_STAMP_RT(P, cond, slot)                                                                       \
   do {                                                                                                      \
-    if ((P).stamps && (cond)) (P).stamps[blockIdx.x * GO2PI_STAMPS_PER_WG + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    if ((P).stamps && (cond))                                                                              \
+      ((__attribute__((address_space(1))) unsigned long long *)(P).stamps)[blockIdx.x * GO2PI_STAMPS_PER_WG + (slot)] = \
+          __builtin_amdgcn_s_memrealtime();                                                                  \
   } while (0)
 #else
 #define GO2PI_STAMP_AT(row, cond, slot) \

@@ -63,13 +63,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define RES_STAMP(i)                                                                        \
   do {                                                                                      \
     if (P.stamps && tid == 0 && (g == 0 || g == 17))                                        \
-      P.stamps[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = wall_clock64();            \
+      ((gu64_t *)P.stamps)[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = wall_clock64();  \
   } while (0)
 // shader-clock stamp beside them (slot i): the clock the request ran at
 #define RES_CLOCK(i)                                                                        \
   do {                                                                                      \
     if (P.stamps && tid == 0 && (g == 0 || g == 17))                                        \
-      P.stamps[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = __builtin_amdgcn_s_memtime(); \
+      ((gu64_t *)P.stamps)[(size_t)(nreq & 511) * 32 + (g ? 16 : 0) + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define RES_STAMP(i) \
@@ -1309,13 +1309,17 @@ __device__ __forceinline__ int a1_poll(const u64 *q, int per, unsigned last, u64
 // A1_STAMP: RESCLK diagnostics, wall clock (slot i) / shader clock (A1_CLOCK) of the
 // first compute lane (tid 64) or, for the poll marks, of the polling wave (tid 0).
 #ifdef GO2PI_DIAG_RESCLK
-#define A1_STAMP(t, i)                                                                           \
-  do {                                                                                           \
-    if (P.stamps && tid == (t)) P.stamps[(size_t)(nreq & 511) * 32 + (i)] = wall_clock64();      \
+// (global stores, not flat: a flat store counts in lgkmcnt too, and every LDS wait after
+// a stamp waited for the stamp's L2 write)
+#define A1_STAMP(t, i)                                                                             \
+  do {                                                                                             \
+    if (P.stamps && tid == (t))                                                                    \
+      ((gu64_t *)P.stamps)[(size_t)(nreq & 511) * 32 + (i)] = wall_clock64();                      \
   } while (0)
-#define A1_CLOCK(t, i)                                                                                        \
-  do {                                                                                                        \
-    if (P.stamps && tid == (t)) P.stamps[(size_t)(nreq & 511) * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+#define A1_CLOCK(t, i)                                                                             \
+  do {                                                                                             \
+    if (P.stamps && tid == (t))                                                                    \
+      ((gu64_t *)P.stamps)[(size_t)(nreq & 511) * 32 + (i)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 #else
 #define A1_STAMP(t, i) \
