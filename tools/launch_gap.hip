@@ -52,5 +52,17 @@ int main() {
     printf("spin %lld cyc 1x64     %.2f us\n", cyc,
            timeit(s, 500, [&] { hipLaunchKernelGGL(spin_k, dim3(1), dim3(64), 0, s, nullptr, cyc); }));
   }
+  // the lean kernel's shape (256 workgroups of 256 threads, ~80K cycles each), on one
+  // stream, then the same launches captured once in a hipGraph and replayed
+  const long long cyc = 80000;
+  const float plain = timeit(s, 500, [&] { hipLaunchKernelGGL(spin_k, dim3(256), dim3(256), 0, s, nullptr, cyc); });
+  printf("spin %lld cyc 256x256  %.2f us\n", cyc, plain);
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+  for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(spin_k, dim3(256), dim3(256), 0, s, nullptr, cyc);
+  hipStreamEndCapture(s, &g);
+  hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  printf("spin %lld cyc 256x256 graph x100  %.2f us\n", cyc, timeit(s, 5, [&] { hipGraphLaunch(ge, s); }) / 100.f);
   return 0;
 }

@@ -15,3 +15,7 @@ tail -2 $O/tests.log
 grep -E "round|p50" $O/lat/ab.txt | tail -18
 timeout -k 10 600 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+if [ -x $R/tools/launch_gap.bin ]; then
+  timeout -k 10 120 $R/tools/launch_gap.bin > $O/launch_gap.txt 2>&1 || { echo "launch_gap failed"; cat $O/launch_gap.txt; exit 1; }
+  cat $O/launch_gap.txt
+fi

@@ -139,7 +139,7 @@ def one_workgroup(args, st, ts, np):
             continue
         cyc[nm] = float(np.median((rows[ok, s_] - prev[ok])))
         prev = np.where(ok, rows[:, s_], prev)
-    out = {"model": args.model, "kernel": "policy_resident1_kernel (one workgroup)",
+    out = {"model": args.model, "kernel": ("policy_resident1_kernel (r04 form, GO2PI_RES_R1W=1)" if os.environ.get("GO2PI_RES_R1W") else "policy_act1_kernel (one workgroup, r05)"),
            "shader_clock_ghz_median": round(float(np.median(ghz)), 3),
            "wave0_cycles_since_previous_mark": cyc,
            "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2], "host_p99_us": ts[int(len(ts) * 0.99)],
