@@ -1046,6 +1046,12 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     // The general body (recurrent policies) takes both only together.
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
     if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
+    // the 8-wave lean kernel (two waves per SIMD) for 512-wide policies: GO2PI_W8=1 (A/B, r05)
+    {
+      const char *w8 = std::getenv("GO2PI_W8");
+      p.w4_nw = (p.w4_tpw == 8 && p.w4_plain && p.w4_actc == 1 && p.w4_nhc == 3 && p.head_fuse <= 1 && w8 &&
+                 w8[0] == '1') ? 8 : 4;
+    }
   }
   // a dense policy whose weights fit one CU's registers is served by the single-
   // workgroup resident kernel (no inter-workgroup hop per layer; GO2PI_RES_MULTI=1:
@@ -1641,7 +1647,10 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     const int c0m = t ? e->prog.w4_c0m : 0;
     if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
                                 // act, hidden layers>
-      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
+      if (e->prog.w4_nw == 8)
+        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 8>", t / 2, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
+      else
+        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
     else
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0, t ? e->prog.w4_actc : -1,

@@ -868,9 +868,10 @@ __device__ __forceinline__ void w4_lds_phase(const float *X, int xs, int lane, i
 // Bounded wait until every OTHER wave has published epoch ep (an LDS word per
 // wave). A protocol failure must not hang the GPU: past the bound the kernel
 // reports through P.err (the engine raises it at the next sync) and goes on.
+template <int NW = 4>
 __device__ __forceinline__ void w4_wait(const int *flags, int wave, int ep, int lane, unsigned *err) {
   for (int it = 0;; ++it) {
-    const int f = lane < 4 && lane != wave ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+    const int f = lane < NW && lane != wave ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)
                                            : ep;
     if (__ballot(f < ep) == 0ull) break;
@@ -1176,6 +1177,7 @@ struct W4Hot {
   float hid_alpha, head_alpha;
   int post_plain;
   float hid_beta, head_beta;
+  int in_dim = 0;  // the lean controller tick (PL && CTL): the observation width, from a preloaded argument
 };
 
 __device__ __forceinline__ W4Hot w4_hot(const DevProgram &P) {
@@ -1198,22 +1200,41 @@ __device__ __forceinline__ void act_dispatch(int act, F &&f) {
 }
 
 // fragments of hidden layer l (l >= 1) of a TPW pipeline (arena layout above)
-template <int TPW>
+template <int TPW, int NW = 4>
 __device__ __forceinline__ const float *w4_layer_w(const W4Hot &h, int l) {
-  constexpr int CH = 4 * TPW;
+  constexpr int CH = NW * TPW;
   return h.l0w + (size_t)(h.c0 + (l - 1) * CH) * CH * 256;
 }
 
 // Layer 0's first RD chunks of the wave's TPW tiles into the register ring (slots
 // K0S ..): the loads w4_step starts a step with.
-template <int TPW, int C0M>
+template <int TPW, int C0M, int NW = 4>
 __device__ __forceinline__ void w4_prefill(const float *l0w, float4 (&f)[4][TPW], int wave, int lane) {
-  constexpr int RD = GO2PI_W4_RD(TPW), CSB = 4 * TPW * 1024, K0S = (4 - C0M) & 3;
+  constexpr int RD = GO2PI_W4_RD(TPW), CSB = NW * TPW * 1024, K0S = (4 - C0M) & 3;
   const WStream w0(l0w);
 #pragma unroll
   for (int d = 0; d < RD; ++d)
 #pragma unroll
     for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = w0.ld(((wave * TPW + i) * 64 + lane) * 16, d * CSB);
+}
+
+// Issue priority of a wave of the 8-wave lean kernel (two waves per SIMD: waves w and
+// w + 4) for phase ph (1: an LDS phase's MFMAs, 0: the epilogue and the own phase).
+// pm 0: none. pm 1: the LDS phase of waves 0-3 ahead of waves 4-7's, both ahead of
+// any epilogue / own phase, so that the two waves of a SIMD finish a contraction
+// apart and one's epilogue runs beside the other's MFMAs. pm 2: LDS phases ahead of
+// epilogue / own phases, no order between the halves. pm 3: waves 0-3 ahead always.
+__device__ __forceinline__ void w4_prio(int pm, int wave, int ph) {
+  if (pm == 1) {
+    if (ph == 0) __builtin_amdgcn_s_setprio(0);
+    else if (wave < 4) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(1);
+  } else if (pm == 2) {
+    if (ph == 0) __builtin_amdgcn_s_setprio(0);
+    else __builtin_amdgcn_s_setprio(1);
+  } else if (pm == 3) {
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
+  }
 }
 
 // One policy step of the pipeline (the observation tile is being staged into bufA).
@@ -1225,14 +1246,20 @@ __device__ __forceinline__ void w4_prefill(const float *l0w, float4 (&f)[4][TPW]
 // a 48- or 98-wide observation padded to 16 rather than 64): layer 0 starts on
 // ring slot (4 - C0M) & 3 so that its last chunk uses slot 3 and layer 1 starts on
 // slot 0 as always.
-template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1, int NHC = 0>
+template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1, int NHC = 0, int NW = 4>
 __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, float *X0, float *Y0, int S,
                                         f32x4 *scratch, int *flags, float *lbias, int &ep, int wave, int lane,
                                         float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
-                                        const CtlLds &CL, int step, const float4 (&ring)[4][TPW], bool pre) {
+                                        const CtlLds &CL, int step, const float4 (&ring)[4][TPW], bool pre,
+                                        int pm = 0) {
   W4Hot hot = hot0;
+  // NW = 8: the issue priority of the two waves of a SIMD per phase (pm, A/B, r05):
+  // ph 1 = an LDS phase's MFMAs, ph 0 = epilogue + own phase (see w4_prio)
+  auto prio = [&](int ph) {
+    if constexpr (NW == 8) w4_prio(pm, wave, ph);
+  };
   constexpr int RD = GO2PI_W4_RD(TPW);
-  constexpr int CH = 4 * TPW;     // k-chunks of every layer after the first (= output tiles of a hidden layer)
+  constexpr int CH = NW * TPW;    // k-chunks of every layer after the first (= output tiles of a hidden layer)
   constexpr int CSB = CH * 1024;  // bytes per k-chunk of a hidden layer's (and layer 0's) fragments
   constexpr int K0S = (4 - C0M) & 3, NT0 = C0M ? C0M : 4;  // layer 0: first ring slot, chunks in its last group
   static_assert(C0M == 0 || C0M == 3, "layer 0 chunk count mod 4");
@@ -1250,14 +1277,14 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   // hidden layers (the fused head follows them); NHC > 0: a compile-time count, the
   // layer loop fully unrolled (a runtime loop carries the ring registers through
   // phi copies at its head, which wait for every fragment load in flight)
-  const int nh = NHC > 0 ? NHC : hot.nbias / (64 * TPW);
+  const int nh = NHC > 0 ? NHC : hot.nbias / (16 * CH);
   int vo[TPW];              // per-lane byte offset of each own tile's fragment in chunk 0 (every layer)
 #pragma unroll
   for (int i = 0; i < TPW; ++i) vo[i] = ((t0 + i) * 64 + lane) * 16;
   // every hidden layer's bias into LDS once, by direct-to-LDS loads in flight with
   // the observation tile's (read per tile by ds_read: off the vmcnt chain of the
   // weight stream, whose waits would otherwise cover them); the head's bias to registers
-  if (step == 0 && !pre) glds_copy(lbias, hot.bpack, hot.nbias, wave, lane, 4);
+  if (step == 0 && !pre) glds_copy(lbias, hot.bpack, hot.nbias, wave, lane, NW);
   float4 hbv[1];  // the head's bias: fetched with the head's fragments (load_head)
   float4 f[4][TPW];
   asm volatile("" ::: "memory");  // the DMA and bias loads stay ahead of the ring's first loads
@@ -1267,7 +1294,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll
       for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = ring[(K0S + d) & 3][i];
   } else {
-    w4_prefill<TPW, C0M>(hot.l0w, f, wave, lane);
+    w4_prefill<TPW, C0M, NW>(hot.l0w, f, wave, lane);
   }
   if constexpr (PL) {
     // the lean kernel: the program's remaining fields are loaded only now, behind the
@@ -1291,7 +1318,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     // (direct-to-LDS, issued at kernel start) and the biases land behind the ring's
     // loads, which stay in flight; then the observation is assembled into X0 and
     // published to the caller's rows, and an LDS-only barrier hands X0 over
-    ctl_here = step == 0 && !P.has_gru;
+    ctl_here = step == 0 && (PL || !P.has_gru);  // (the lean kernel has no recurrent cell)
     if (ctl_here) {
       const CtlQ cq = ctl_q(P, ctl);  // (its scalar loads land behind the barrier's wait)
       // r05: two waits. The direct-to-LDS loads went out as q0 | state, joystick and
@@ -1301,12 +1328,13 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       // rows are assembled while the observation rows land; the
       // second (inside the assembly) waits for those before vel_cmd and the shift pass.
       const int nrows = min(GO2PI_TILE_ROWS, B - row0);
-      const int later = glds_count(nrows * P.in_dim, wave, 4) + (step == 0 && !pre ? glds_count(hot.nbias, wave, 4) : 0);
+      const int ind = PL ? hot.in_dim : P.in_dim;  // (the lean tick: no program round trip in front of the wait)
+      const int later = glds_count(nrows * ind, wave, NW) + (step == 0 && !pre ? glds_count(hot.nbias, wave, NW) : 0);
       vm_wait_rt(later + RD * TPW);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       GO2PI_STAMP(P, threadIdx.x == 0, 5);
       ctl_assemble_split<true>(P, CL, cq, ctl.joy != nullptr, nrows, X0, S, ctl.obs + (size_t)row0 * P.in_dim,
-                               threadIdx.x, 256, [] { wg_barrier_vm<RD * TPW>(); });
+                               threadIdx.x, NW * 64, [] { wg_barrier_vm<RD * TPW>(); });
       lds_barrier();
     }
   }
@@ -1339,8 +1367,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   for (int i = 0; i < TPW; ++i) acc[i] = BIN ? f32x4{bv[i].x, bv[i].y, bv[i].z, bv[i].w} : f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const WStream ws(hot.l0w);
+    prio(1);
     if (nh > 1) {
-      const WStream wn(w4_layer_w<TPW>(hot, 1));
+      const WStream wn(w4_layer_w<TPW, NW>(hot, 1));
       w4_lds_phase<TPW, RD, K0S, NT0, true>(X0, S, lane, hot.c0, 0, 0, ws, CSB, wn, CSB, kb1, CH, vo, acc, f);
     } else {
       w4_lds_phase<TPW, RD, K0S, NT0, false>(X0, S, lane, hot.c0, 0, 0, ws, CSB, ws, 0, 0, 1, vo, acc, f);
@@ -1356,7 +1385,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll kHidUnroll
   for (int l = 1; l < nh; ++l) {
     const bool more = l + 1 < nh;
-    const WStream ws(w4_layer_w<TPW>(hot, l)), wn(w4_layer_w<TPW>(hot, more ? l + 1 : l));
+    const WStream ws(w4_layer_w<TPW, NW>(hot, l)), wn(w4_layer_w<TPW, NW>(hot, more ? l + 1 : l));
     float4 bvn[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) bvn[i] = *reinterpret_cast<const float4 *>(brow + l * CH * 16 + i * 16);
@@ -1373,6 +1402,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     };
     // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
     [[maybe_unused]] const bool sub = lane == 0 && step == 0 && l == 1;
+    prio(0);
     {
     // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
     // publish, then layer l's MFMAs over those chunks with the B operand from registers
@@ -1410,8 +1440,9 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     if constexpr (!HO) __syncthreads();
     }
     GO2PI_STAMP(P, sub, 28 + 3 * wave);
-    if constexpr (HO) w4_wait(flags, wave, ep, lane, hot.err);
+    if constexpr (HO) w4_wait<NW>(flags, wave, ep, lane, hot.err);
     GO2PI_STAMP(P, sub, 29 + 3 * wave);
+    prio(1);
     // LDS phase: the other waves' chunks, rotated order from t0 + TPW
     constexpr int K0 = HO ? TPW : 0;                             // first chunk index of the LDS phase
     constexpr int NT = (CH - K0) % 4 ? (CH - K0) % 4 : 4;       // chunks in the LDS phase's last group
@@ -1442,6 +1473,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     for (int h = 0; h < HT; ++h)
 #pragma unroll
       for (int c = 0; c < NCH; ++c) hacc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    prio(0);
     act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
 #pragma unroll
@@ -1463,20 +1495,20 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     for (int h = 0; h < HT; ++h) {
       f32x4 t = hacc[h][0] + hacc[h][1];
       if constexpr (NCH == 4) t = t + (hacc[h][2] + hacc[h][3]);
-      scratch[(h * 4 + wave) * 64 + lane] = t;
+      scratch[(h * NW + wave) * 64 + lane] = t;
     }
   }
   __syncthreads();
   GO2PI_STAMP(P, threadIdx.x == 0 && step == 0 && nh < 9, 6 + nh);
   if (wave < HT) {  // head tile `wave`: the four waves' partials in a fixed order, bias, final store
-    f32x4 hs[1] = {scratch[(wave * 4) * 64 + lane]};
+    f32x4 hs[1] = {scratch[(wave * NW) * 64 + lane]};
 #pragma unroll
-    for (int w = 1; w < 4; ++w) hs[0] += scratch[(wave * 4 + w) * 64 + lane];
+    for (int w = 1; w < NW; ++w) hs[0] += scratch[(wave * NW + w) * 64 + lane];
     GO2PI_STAMP(P, lane == 0 && wave == 0 && step == 0, 54);  // tail marks: 54 partials summed, 55 stored
     // no action post-processing (the lean kernel; a general-body program without
     // tanh / clip / scale, e.g. a GRU policy): the head's activation (usually none)
     // and the plain store of the valid rows / columns, from the hot fields
-    if (PL || (!CTL && hot.post_plain)) {
+    if (!CTL && (PL || hot.post_plain)) {
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
       with_act(hot.head_act, [&](auto act_k) {
         constexpr int ACT = decltype(act_k)::value;
@@ -1508,10 +1540,10 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 // fragment loads issue at wave start with no memory round trip in front of them
 // (each dependent load at kernel start costs ~1.5K cycles: the L2s are cold), and
 // the rest of the program's hot block is loaded beside them, needed only later.
-// dims = in_dim | c0 << 12 | hidden layers << 20. The LDS stride is a
+// dims = in_dim | c0 << 12 | hidden layers << 20 | w4_prio mode << 28. The LDS stride is a
 // compile-time constant; padding lanes of the observation tile read an element of
 // the same row (times a zero weight column), rows past B the last row.
-template <int TPW, int HT, int C0M, int ACTC, int NHC>
+template <int TPW, int HT, int C0M, int ACTC, int NHC, int NW = 4>
 __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *__restrict__ obs,
                                               float *__restrict__ act, const float *l0w, const float *bpack, int B,
                                               int steps, unsigned dims, unsigned *yield) {
@@ -1520,13 +1552,14 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   // tell idle resident kernels on this device to give their CUs back (resident.hip)
   if (blockIdx.x == 0 && threadIdx.x == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)(dims >> 20);
+  const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)((dims >> 20) & 0xFFu);
+  const int pm = (int)(dims >> 28);  // (NW = 8: the priority mode, w4_prio)
   // (the program's fields are read inside w4_step once the first loads are out)
-  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 64 * TPW, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
-  constexpr int S = 64 * TPW + 4;  // = P.lds_stride (the engine selects this kernel only then)
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 16 * NW * TPW, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
+  constexpr int S = 16 * NW * TPW + 4;  // = P.lds_stride (the engine selects this kernel only then)
   float *bufA = lds, *bufB = lds + GO2PI_TILE_ROWS * S;
   f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + 2 * GO2PI_TILE_ROWS * S);
-  int *flags = reinterpret_cast<int *>(lds + 2 * GO2PI_TILE_ROWS * S + 256 * 4 * HT);
+  int *flags = reinterpret_cast<int *>(lds + 2 * GO2PI_TILE_ROWS * S + 256 * NW * HT);
   float *lbias = reinterpret_cast<float *>(flags) + GO2PI_FLAG_FLOATS;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1535,25 +1568,72 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   int ep = 0;                           // flag epochs published so far (the same in every wave)
   float4 ring_none[4][TPW];             // (w4_step loads its own ring here)
   for (int step = 0; step < steps; ++step) {
-    // wave w stages rows w, w + 4, w + 8, w + 12 in whole 64-column chunks by
-    // direct-to-LDS loads
+    // wave w stages rows w, w + NW, ... in whole 64-column chunks by direct-to-LDS
+    // loads
     const float *ob = obs + (size_t)step * B * in_dim;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wave + 4 * i, row = min(row0 + r, B - 1);
+    for (int i = 0; i < GO2PI_TILE_ROWS / NW; ++i) {
+      const int r = wave + NW * i, row = min(row0 + r, B - 1);
       const float *rp = ob + (size_t)row * in_dim;
       for (int c = 0; c < nch; ++c)
         __builtin_amdgcn_global_load_lds((gvoid_t *)(rp + min(c * 64 + lane, in_dim - 1)),
                                          (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
     }
-    if (step == 0 && tid < 4) flags[tid] = 0;
+    if (step == 0 && tid < NW) flags[tid] = 0;
     GO2PI_STAMP(P, tid == 0 && step == 0, 0);
     GO2PI_STAMP_RT(P, tid == 0 && step == 0, 1);
     GO2PI_STAMP(P, tid == 0 && step == 0, 40);
     GO2PI_STAMP(P, tid == 0 && step == 0, 41);
-    w4_step<TPW, HT, false, true, C0M, ACTC, NHC>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
-                                       CtlLds{}, step, ring_none, false);
+    w4_step<TPW, HT, false, true, C0M, ACTC, NHC, NW>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
+                                       CtlLds{}, step, ring_none, false, pm);
   }
+  GO2PI_STAMP(P, tid == 0, 2);
+  GO2PI_STAMP_RT(P, tid == 0, 3);
+}
+
+// The lean controller tick (r05): the controller prologue and
+// epilogue (ctl_fn.hpp) around the lean pipeline, for a dense policy with the
+// compile-time Elu and three hidden layers. Everything the input staging needs
+// arrives as kernel arguments preloaded into SGPRs: the tile's state, joystick,
+// previous observation and previous action rows and the controller parameters (q0)
+// go out as direct-to-LDS loads in the first ~200 cycles, where the general body
+// issued them ~2.7K cycles in, behind the chain kernel argument -> program -> its
+// fields (profiles/r05_clock_ctl.json, init_subphases.obs_issued). The rest of the
+// program and the controller arguments are read behind those loads.
+// shape = B | in_dim << 20 (B < 2^20, in_dim < 2^12: the engine checks).
+template <int TPW, int HT, int C0M>
+__device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &ctl, const float *l0w,
+                                            const float *bpack, unsigned shape, unsigned *yield) {
+  extern __shared__ float4 lds4[];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const int B = (int)(shape & 0xFFFFFu), in_dim = (int)(shape >> 20);
+  constexpr int S = 64 * TPW + 4, NBIAS = 3 * 64 * TPW;  // (three hidden layers, NHC = 3)
+  float *bufA = lds, *bufB = lds + GO2PI_TILE_ROWS * S;
+  f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + 2 * GO2PI_TILE_ROWS * S);
+  int *flags = reinterpret_cast<int *>(lds + 2 * GO2PI_TILE_ROWS * S + 256 * 4 * HT);
+  float *lbias = reinterpret_cast<float *>(flags) + GO2PI_FLAG_FLOATS;
+  // (the previous observation rows in bufB: layer 0's output buffer, written only after
+  // the assembly and the barrier behind it; as fused_body)
+  const CtlLds CL = ctl_lds(lbias + NBIAS, GO2PI_TILE_ROWS, in_dim, bufB);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
+  ctl_lds_load(CL, ctl, row0, min(GO2PI_TILE_ROWS, B - row0), in_dim, tid, wave, lane, 4);
+  if (tid < 4) flags[tid] = 0;
+  // tell idle resident kernels on this device to give their CUs back (resident.hip),
+  // behind the staging loads
+  if (blockIdx.x == 0 && tid == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
+    __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  GO2PI_STAMP(P, tid == 0, 0);
+  GO2PI_STAMP_RT(P, tid == 0, 1);
+  GO2PI_STAMP(P, tid == 0, 41);
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, (in_dim + 15) >> 4, 0, 0,
+                          0.f, 0.f, 1, 0.f, 0.f, in_dim};
+  const CtlView cv = ctl_view(ctl, CL, row0);
+  int ep = 0;
+  float4 ring_none[4][TPW];  // (w4_step loads its own ring here)
+  w4_step<TPW, HT, true, true, C0M, 1, 3>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, nullptr, cv,
+                                          row0, B, ctl, CL, 0, ring_none, false);
   GO2PI_STAMP(P, tid == 0, 2);
   GO2PI_STAMP_RT(P, tid == 0, 3);
 }
@@ -1888,19 +1968,43 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_kernel(const DevProgram 
 // The lean pipeline kernel (w4_plain_body). Argument order = preload order: the
 // first 16 dwords of the kernel arguments arrive in SGPRs (kernels_w4_t*.hip are
 // built with -amdgpu-kernarg-preload-count=16); these are 13.
-template <int TPW, int HT, int C0M, int ACTC, int NHC>
-__global__ __launch_bounds__(256) void policy_mlp_kernel(const float *__restrict__ obs, float *__restrict__ act,
-                                                         const float *__restrict__ l0w,
-                                                         const float *__restrict__ bpack,
-                                                         const DevProgram *__restrict__ Pd, int B, int steps,
-                                                         unsigned dims, unsigned *yield) {
-  w4_plain_body<TPW, HT, C0M, ACTC, NHC>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
+// NW: waves per workgroup, 4 (one per SIMD, the r01-r04 pipeline) or 8 (two per SIMD,
+// TPW tiles each: while one wave of a SIMD runs its epilogue, the other's MFMAs keep
+// the matrix pipe busy; tools/mfma_2wave.hip: a partner wave's epilogue VALU leaves
+// the MFMA wave's 32 cycles per v_mfma_f32_16x16x4_f32 untouched, r05).
+template <int TPW, int HT, int C0M, int ACTC, int NHC, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void policy_mlp_kernel(const float *__restrict__ obs, float *__restrict__ act,
+                                                             const float *__restrict__ l0w,
+                                                             const float *__restrict__ bpack,
+                                                             const DevProgram *__restrict__ Pd, int B, int steps,
+                                                             unsigned dims, unsigned *yield) {
+  w4_plain_body<TPW, HT, C0M, ACTC, NHC, NW>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>
 __global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(const DevProgram *__restrict__ Pd, DevCtl C,
                                                                    float *__restrict__ hidden, int B) {
   fused_body<NW, true, W4T, W4H, C0M, RNN>(*Pd, nullptr, nullptr, hidden, B, 1, C);
+}
+
+// The lean controller tick (w4_ctl_body). The first arguments, up to shape, are
+// preloaded into SGPRs (13 dwords); C (its row pointers repeat the preloaded ones),
+// Pd and yield come from the kernel argument segment, needed only later.
+template <int TPW, int HT, int C0M>
+__global__ __launch_bounds__(256) void policy_mlp_ctl_kernel(const float *__restrict__ state,
+                                                             const float *__restrict__ joy, float *__restrict__ obs,
+                                                             float *__restrict__ act, const DevCtlParams *prm,
+                                                             const float *__restrict__ l0w, unsigned shape,
+                                                             const float *__restrict__ bpack,
+                                                             const DevProgram *__restrict__ Pd, unsigned *yield,
+                                                             DevCtl C) {
+  DevCtl c = C;
+  c.state = state;
+  c.joy = joy;
+  c.obs = obs;
+  c.action = act;
+  c.prm = prm;
+  w4_ctl_body<TPW, HT, C0M>(*Pd, c, l0w, bpack, shape, yield);
 }
 
 }  // namespace go2pi
