@@ -1218,25 +1218,6 @@ __device__ __forceinline__ void w4_prefill(const float *l0w, float4 (&f)[4][TPW]
     for (int i = 0; i < TPW; ++i) f[(K0S + d) & 3][i] = w0.ld(((wave * TPW + i) * 64 + lane) * 16, d * CSB);
 }
 
-// Issue priority of a wave of the 8-wave lean kernel (two waves per SIMD: waves w and
-// w + 4) for phase ph (1: an LDS phase's MFMAs, 0: the epilogue and the own phase).
-// pm 0: none. pm 1: the LDS phase of waves 0-3 ahead of waves 4-7's, both ahead of
-// any epilogue / own phase, so that the two waves of a SIMD finish a contraction
-// apart and one's epilogue runs beside the other's MFMAs. pm 2: LDS phases ahead of
-// epilogue / own phases, no order between the halves. pm 3: waves 0-3 ahead always.
-__device__ __forceinline__ void w4_prio(int pm, int wave, int ph) {
-  if (pm == 1) {
-    if (ph == 0) __builtin_amdgcn_s_setprio(0);
-    else if (wave < 4) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(1);
-  } else if (pm == 2) {
-    if (ph == 0) __builtin_amdgcn_s_setprio(0);
-    else __builtin_amdgcn_s_setprio(1);
-  } else if (pm == 3) {
-    if (wave < 4) __builtin_amdgcn_s_setprio(1);
-  }
-}
-
 // One policy step of the pipeline (the observation tile is being staged into bufA).
 // pre: the ring already filled by w4_prefill and the biases' direct-to-LDS copy
 // already issued (a recurrent policy does both behind its cell's contraction).
@@ -1250,14 +1231,8 @@ template <int TPW, int HT, bool CTL, bool PL, int C0M, int ACTC = -1, int NHC = 
 __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, float *X0, float *Y0, int S,
                                         f32x4 *scratch, int *flags, float *lbias, int &ep, int wave, int lane,
                                         float *ac, const CtlView cv, int row0, int B, const DevCtl &ctl,
-                                        const CtlLds &CL, int step, const float4 (&ring)[4][TPW], bool pre,
-                                        int pm = 0) {
+                                        const CtlLds &CL, int step, const float4 (&ring)[4][TPW], bool pre) {
   W4Hot hot = hot0;
-  // NW = 8: the issue priority of the two waves of a SIMD per phase (pm, A/B, r05):
-  // ph 1 = an LDS phase's MFMAs, ph 0 = epilogue + own phase (see w4_prio)
-  auto prio = [&](int ph) {
-    if constexpr (NW == 8) w4_prio(pm, wave, ph);
-  };
   constexpr int RD = GO2PI_W4_RD(TPW);
   constexpr int CH = NW * TPW;    // k-chunks of every layer after the first (= output tiles of a hidden layer)
   constexpr int CSB = CH * 1024;  // bytes per k-chunk of a hidden layer's (and layer 0's) fragments
@@ -1340,7 +1315,12 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   }
   // layer 0's input rows are complete in X0 and the biases in LDS (this wave's
   // direct-to-LDS loads, older than the ring's); the ring's loads stay in flight
-  if (!ctl_here) wg_barrier_vm<RD * TPW>();
+  // (NW = 8: vmcnt(0). The count RD * TPW assumes the ring's loads were issued after
+  // the staging loads, but loads through a __restrict__ const pointer are invariant and
+  // the compiler may sink them below this barrier: with run-time branches after it (an
+  // r05 issue-priority experiment) it did, vmcnt(RD * TPW) waited for nothing, and rows
+  // staged by waves 4-7 were read before they landed.)
+  if (!ctl_here) wg_barrier_vm<NW == 8 ? 0 : RD * TPW>();
   GO2PI_STAMP(P, threadIdx.x == 0 && step == 0, 4);
   if constexpr (CTL) {
     if (ctl.status && (int)threadIdx.x < min(GO2PI_TILE_ROWS, B - row0)) ctl.status[row0 + threadIdx.x] = CL.nanf[threadIdx.x];
@@ -1367,7 +1347,6 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
   for (int i = 0; i < TPW; ++i) acc[i] = BIN ? f32x4{bv[i].x, bv[i].y, bv[i].z, bv[i].w} : f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const WStream ws(hot.l0w);
-    prio(1);
     if (nh > 1) {
       const WStream wn(w4_layer_w<TPW, NW>(hot, 1));
       w4_lds_phase<TPW, RD, K0S, NT0, true>(X0, S, lane, hot.c0, 0, 0, ws, CSB, wn, CSB, kb1, CH, vo, acc, f);
@@ -1402,7 +1381,6 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     };
     // layer 1 sub-phases per wave: 28 + 3w + {own phase done, wait done, LDS phase done}
     [[maybe_unused]] const bool sub = lane == 0 && step == 0 && l == 1;
-    prio(0);
     {
     // own phase: layer l-1's epilogue for all the wave's tiles (to registers and LDS),
     // publish, then layer l's MFMAs over those chunks with the B operand from registers
@@ -1442,7 +1420,6 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     GO2PI_STAMP(P, sub, 28 + 3 * wave);
     if constexpr (HO) w4_wait<NW>(flags, wave, ep, lane, hot.err);
     GO2PI_STAMP(P, sub, 29 + 3 * wave);
-    prio(1);
     // LDS phase: the other waves' chunks, rotated order from t0 + TPW
     constexpr int K0 = HO ? TPW : 0;                             // first chunk index of the LDS phase
     constexpr int NT = (CH - K0) % 4 ? (CH - K0) % 4 : 4;       // chunks in the LDS phase's last group
@@ -1473,7 +1450,6 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     for (int h = 0; h < HT; ++h)
 #pragma unroll
       for (int c = 0; c < NCH; ++c) hacc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    prio(0);
     act_dispatch<ACTC>(hot.hid_act, [&](auto act_k) {
       constexpr int ACT = decltype(act_k)::value;
 #pragma unroll
@@ -1540,7 +1516,7 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 // fragment loads issue at wave start with no memory round trip in front of them
 // (each dependent load at kernel start costs ~1.5K cycles: the L2s are cold), and
 // the rest of the program's hot block is loaded beside them, needed only later.
-// dims = in_dim | c0 << 12 | hidden layers << 20 | w4_prio mode << 28. The LDS stride is a
+// dims = in_dim | c0 << 12 | hidden layers << 20. The LDS stride is a
 // compile-time constant; padding lanes of the observation tile read an element of
 // the same row (times a zero weight column), rows past B the last row.
 template <int TPW, int HT, int C0M, int ACTC, int NHC, int NW = 4>
@@ -1553,7 +1529,6 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
   if (blockIdx.x == 0 && threadIdx.x == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int in_dim = (int)(dims & 0xFFFu), c0 = (int)((dims >> 12) & 0xFFu), nh = (int)((dims >> 20) & 0xFFu);
-  const int pm = (int)(dims >> 28);  // (NW = 8: the priority mode, w4_prio)
   // (the program's fields are read inside w4_step once the first loads are out)
   const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, nh * 16 * NW * TPW, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
   constexpr int S = 16 * NW * TPW + 4;  // = P.lds_stride (the engine selects this kernel only then)
@@ -1585,7 +1560,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
     GO2PI_STAMP(P, tid == 0 && step == 0, 40);
     GO2PI_STAMP(P, tid == 0 && step == 0, 41);
     w4_step<TPW, HT, false, true, C0M, ACTC, NHC, NW>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
-                                       CtlLds{}, step, ring_none, false, pm);
+                                       CtlLds{}, step, ring_none, false);
   }
   GO2PI_STAMP(P, tid == 0, 2);
   GO2PI_STAMP_RT(P, tid == 0, 3);
