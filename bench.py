@@ -313,7 +313,7 @@ def controller_leg(device, steps=200, warm=20, iters=10000):
 
 def load_pmc(workload, kernel):
     """(bytes, note): memory-side bytes per launch of the batched kernel
-    instantiation `kernel` (e.g. "policy_mlp_kernel<8, 1, 3, 1, 3>",
+    instantiation `kernel` (e.g. "policy_mlp_kernel<8, 1, 3, 1, 3, 4>",
     Engine.batched_kernel) from the committed rocprofv3 --pmc summary of this
     workload (tools/profile.sh + tools/summarize_prof.py: separate FETCH_SIZE /
     WRITE_SIZE passes, gfx950 read correction x2), and where it came from. bytes is

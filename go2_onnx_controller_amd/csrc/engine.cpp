@@ -1647,10 +1647,11 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     const int c0m = t ? e->prog.w4_c0m : 0;
     if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
                                 // act, hidden layers>
+      // (<..., waves per workgroup>: 4, or 8 with half the tiles per wave)
       if (e->prog.w4_nw == 8)
         std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 8>", t / 2, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
       else
-        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
+        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 4>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
     else
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0, t ? e->prog.w4_actc : -1,

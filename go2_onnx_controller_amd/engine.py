@@ -206,7 +206,7 @@ class Engine:
         if hasattr(L, "go2pi_batched_kernel") and L.go2pi_batched_kernel.argtypes:
             kb = ctypes.create_string_buffer(128)
             _check(L.go2pi_batched_kernel(h, kb, 128))
-            self.batched_kernel = kb.value.decode()  # e.g. "policy_mlp_kernel<8, 1, 3, 1, 3>" (rocprofv3 name)
+            self.batched_kernel = kb.value.decode()  # e.g. "policy_mlp_kernel<8, 1, 3, 1, 3, 4>" (rocprofv3 name)
 
     def _io(self, is_out, k):
         L = lib()

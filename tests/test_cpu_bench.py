@@ -56,7 +56,7 @@ def test_traffic_null_when_profile_is_stale(tmp_path, monkeypatch):
     sys.path.insert(0, ROOT)
     import bench
     from go2_onnx_controller_amd.provenance import kernel_source_digest
-    kern = "policy_mlp_kernel<8, 1, 3, 1, 3>"
+    kern = "policy_mlp_kernel<8, 1, 3, 1, 3, 4>"
     name = f"void go2pi::{kern}(go2pi::DevProgram const*, float const*, float*, int)"
     (tmp_path / "profiles").mkdir()
     summary = tmp_path / "profiles" / "pmc_summary.json"

@@ -21,15 +21,15 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 # instantiation names: policy_mlp_kernel<tiles per wave, head tiles, layer-0 chunks mod 4, hidden
-# activation (1 Elu compile-time, -1 runtime), hidden layers (3 compile-time, 0 runtime)> (the lean body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
+# activation (1 Elu compile-time, -1 runtime), hidden layers (3 compile-time, 0 runtime), waves> (the lean body) or policy_fused_kernel<waves, tiles per wave, head tiles, layer-0 chunks mod 4,
 # recurrent cell (0 none / GRU, 1 LSTM), act, hidden layers>
 # (a 33-, 40- or 48-wide observation is padded to 48 columns: 3 chunks; 70 to 128)
 SHAPES = {
-    "pipe_512_relu": "policy_mlp_kernel<8, 1, 0, -1, 0>",
-    "pipe_256_h2": "policy_mlp_kernel<4, 2, 3, 1, 0>",
-    "pipe_128_tanh_h2": "policy_mlp_kernel<2, 2, 3, -1, 0>",
-    "pipe_one_hidden": "policy_mlp_kernel<4, 1, 3, 1, 0>",
-    "go2_mlp_512": "policy_mlp_kernel<8, 1, 3, 1, 3>",
+    "pipe_512_relu": "policy_mlp_kernel<8, 1, 0, -1, 0, 4>",
+    "pipe_256_h2": "policy_mlp_kernel<4, 2, 3, 1, 0, 4>",
+    "pipe_128_tanh_h2": "policy_mlp_kernel<2, 2, 3, -1, 0, 4>",
+    "pipe_one_hidden": "policy_mlp_kernel<4, 1, 3, 1, 0, 4>",
+    "go2_mlp_512": "policy_mlp_kernel<8, 1, 3, 1, 3, 4>",
 }
 
 
