@@ -1492,9 +1492,13 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
         if (row < B) {  // (lean kernel: ac = the action rows of all steps, this step's at step * B
                         // rows; general body: ac = this step's rows already)
           float *o = ac + ((PL ? (size_t)step * B : (size_t)0) + row) * hot.head_n;
+          if ((hot.head_n & 3) == 0 && ((uintptr_t)ac & 15) == 0) {  // (12 actions: one 16-byte store per lane)
+            if (n0 < hot.head_n) *reinterpret_cast<float4 *>(o + n0) = v;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n0 + r < hot.head_n) o[n0 + r] = f4c(v, r);
+            for (int r = 0; r < 4; ++r)
+              if (n0 + r < hot.head_n) o[n0 + r] = f4c(v, r);
+          }
         }
       });
     } else {
@@ -1634,6 +1638,18 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   if (blockIdx.x == 0 && tid == 0 && P.yield && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(P.yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int H = P.gru.H, SW = P.gru.sw;  // hidden width; state floats per robot (LSTM: h | c)
+  // (r05) the program fields read between the first direct-to-LDS load and the recurrent
+  // cell's contraction, read once here, before any. The compiler models a direct-to-LDS
+  // load as a store to memory, so a program field read after one waited vmcnt(0), the
+  // staging loads' whole HBM round trip, each time: GRU-256 tick, observation loads
+  // issued at 1.9K cycles, hidden rows at 3.9K, the cell entered at 6.6K
+  // (profiles/r05_clock_gru256.json, slots 41, 56, 58)
+  const int zero_fill = P.zero_fill, has_gru = P.has_gru, out_dim = P.out_dim, in_dim0 = P.in_dim,
+            in_pad0 = P.in_pad;
+  const float *pzero = P.zero;
+  const DevGru G = P.gru;
+  const float *w4_bpack = P.w4_bpack, *l0_w = P.l0_w;
+  const int w4_bias = P.w4_bias;
   // Touch every layer descriptor up front: one burst of scalar loads warms the
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
@@ -1693,9 +1709,9 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       // chunks (in_pad is a GRU's input width, not always a multiple of 64);
       // per-lane source pointers are formed once, so the loop carries no scalar
       // reloads between the direct-to-LDS loads
-      const int in_dim = P.in_dim, nch = (P.in_pad + 63) >> 6;
+      const int in_dim = in_dim0, nch = (in_pad0 + 63) >> 6;
       const float *ob = obs + (size_t)step * B * in_dim;
-      const float *zero = P.zero + lane;
+      const float *zero = pzero + lane;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wave + 4 * i, row = row0 + r;
@@ -1731,29 +1747,29 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // observation does not cover, once.
   stage_obs(0);
   GO2PI_STAMP(P, tid == 0, 41);
-  if (P.zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
+  if (zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int tail4 = (S - P.in_pad) >> 2;
+    const int tail4 = (S - in_pad0) >> 2;
     for (int e = tid; e < GO2PI_TILE_ROWS * tail4; e += NT) {
       const int r = e / tail4;
-      reinterpret_cast<float4 *>(bufA + r * S + P.in_pad)[e - r * tail4] = z;
+      reinterpret_cast<float4 *>(bufA + r * S + in_pad0)[e - r * tail4] = z;
     }
     if constexpr (CTL) __syncthreads();  // every wave done reading the previous observation rows in bufB
     float4 *l4 = reinterpret_cast<float4 *>(bufB);
-    const int n4 = ((1 + P.has_gru) * GO2PI_TILE_ROWS * S) >> 2;
+    const int n4 = ((1 + has_gru) * GO2PI_TILE_ROWS * S) >> 2;
     for (int e = tid; e < n4; e += NT) l4[e] = z;
   }
-  if (P.has_gru) {
+  if (has_gru) {
     // the zero fill above before the hidden rows land (otherwise no barrier: the
     // hidden rows' direct-to-LDS loads go out beside the observation's)
-    if (P.zero_fill) __syncthreads();
+    if (zero_fill) __syncthreads();
     if (W4T > 0 && H % 64 == 0) {
       // pipeline: the hidden rows by direct-to-LDS loads, in flight with the
       // observation's (one 64-column chunk per instruction; rows past B read zeros)
       for (int i = 0; i < 4; ++i) {
         const int r = wave + 4 * i, row = row0 + r;
         for (int c = 0; c < (H >> 6); ++c) {
-          const float *src = row < B ? hidden + (size_t)row * SW + c * 64 + lane : P.zero + lane;
+          const float *src = row < B ? hidden + (size_t)row * SW + c * 64 + lane : pzero + lane;
           __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)(bufH + r * S + c * 64), 4, 0, 0);
         }
       }
@@ -1764,9 +1780,10 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       }
     }
   }
+  GO2PI_STAMP(P, tid == 0 && has_gru, 56);  // (GRU prologue marks: 56 hidden rows issued, 57 step loop, 58 cell entry)
   // LSTM, pipeline: this lane's cell-state units (w4_lstm) in registers for the whole sequence
   float4 creg[4];
-  if (RNN == 1 && W4T > 0 && P.has_gru && (H == 256 || H == 128)) {
+  if (RNN == 1 && W4T > 0 && has_gru && (H == 256 || H == 128)) {
     const int GT = H >> 6, row = row0 + (lane & 15);
     const float *cg = hidden + (size_t)row * SW + H + wave * GT * 16 + ((lane >> 4) << 2);
 #pragma unroll
@@ -1774,14 +1791,15 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       creg[i] = (i < GT && row < B) ? *reinterpret_cast<const float4 *>(cg + i * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   for (int step = 0; step < steps; ++step) {
-    float *ac = act + (size_t)step * B * P.out_dim;
+    float *ac = act + (size_t)step * B * out_dim;
+    GO2PI_STAMP(P, tid == 0 && step == 0 && has_gru, 57);
     if (step > 0) stage_obs(step);
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
       float *X0 = bufA, *Y0 = bufB;
       float4 ring0[4][W4T > 0 ? W4T : 1];  // layer 0's ring, filled behind a recurrent cell (w4_prefill)
       bool ring_pre = false;
-      if (P.has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
+      if (has_gru) {  // recurrent policy: the GRU cell first, h' is the pipeline's input
         // the pipelined cell (w4_gru / w4_lstm wait for the x / h staging and barrier
         // themselves): h' to bufB, registers, and the carry
         auto carry = [&](auto gt_k) {
@@ -1796,19 +1814,20 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
           constexpr bool PREF = !(lstm && ACTC != 1);
           auto mid = [&] {
             if constexpr (PREF) {
-              if (step == 0) glds_copy(lbias, P.w4_bpack, P.w4_bias, wave, lane, 4);
-              w4_prefill<W4T, C0M>(P.l0_w, ring0, wave, lane);
+              if (step == 0) glds_copy(lbias, w4_bpack, w4_bias, wave, lane, 4);
+              w4_prefill<W4T, C0M>(l0_w, ring0, wave, lane);
             }
           };
+          GO2PI_STAMP(P, tid == 0 && step == 0, 58);
           if constexpr (lstm) {
             float4 cr[GT];
 #pragma unroll
             for (int i = 0; i < GT; ++i) cr[i] = creg[i];
-            w4_lstm<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn, cr, mid);
+            w4_lstm<GT>(G, bufA, bufH, bufB, S, wave, lane, hn, cr, mid);
 #pragma unroll
             for (int i = 0; i < GT; ++i) creg[i] = cr[i];
           } else {
-            w4_gru<GT>(P.gru, bufA, bufH, bufB, S, wave, lane, hn,
+            w4_gru<GT>(G, bufA, bufH, bufB, S, wave, lane, hn,
                        P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, mid);
           }
           ring_pre = PREF;

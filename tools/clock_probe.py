@@ -87,6 +87,9 @@ def main():
         gru_sub = {"entry": float(np.median(st[:, 43] - st[:, 0])),
                    "contraction": float(np.median(st[:, 44] - st[:, 43])),
                    "epilogue": float(np.median(st[:, 45] - st[:, 44]))}
+        for slot, name in ((56, "prologue_hidden_issued"), (57, "prologue_step_loop"), (58, "prologue_cell_call")):
+            if np.all(st[:, slot] > 0):
+                gru_sub[name] = float(np.median(st[:, slot] - st[:, 0]))
     blocks = {}
     if args.ctl and np.all(st[:, 51] > 0):  # the assembly's passes (slots 50-51, thread 0) from slot 5
         prev = st[:, 5]
