@@ -160,6 +160,15 @@ __device__ __forceinline__ CtlQ ctl_q(const DevProgram &P, const DevCtl C) {
               pro_of(P)};
 }
 
+// The lean tick's CtlQ (w4_ctl_body): a program with no observation prologue, so no
+// program field is read. A program field read after the tile's direct-to-LDS loads is
+// a vector load queued behind them (the loads are modelled as stores), and its wait
+// would be a wait for every one of them.
+__device__ __forceinline__ CtlQ ctl_q_plain(const DevCtl C, int in_dim, int in_pad) {
+  kparams_t &Q = *(kparams_t *)C.prm;
+  return CtlQ{Q.hist, Q.contact_threshold, Q.gravity_w[0], Q.gravity_w[1], Q.gravity_w[2], in_dim, in_pad, Pro{}};
+}
+
 // Block b of the 49 values a tick appends per robot (controller.cpp:210-212):
 // 0 gravity_b 3, 1 base_ang_vel 3, 2 vel_cmd 3, 3 q - q0 12, 4 dq 12, 5 action 12,
 // 6 contacts 4. cum: the block's first value among the 49; d: its width. In the

@@ -1295,7 +1295,8 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     // published to the caller's rows, and an LDS-only barrier hands X0 over
     ctl_here = step == 0 && (PL || !P.has_gru);  // (the lean kernel has no recurrent cell)
     if (ctl_here) {
-      const CtlQ cq = ctl_q(P, ctl);  // (its scalar loads land behind the barrier's wait)
+      // (the lean tick: no program field, ctl_q_plain; otherwise its loads land behind the wait)
+      const CtlQ cq = PL ? ctl_q_plain(ctl, hot.in_dim, 16 * hot.c0) : ctl_q(P, ctl);
       // r05: two waits. The direct-to-LDS loads went out as q0 | state, joystick and
       // action rows | previous observation rows (ctl_lds_load) | the hidden biases, then
       // the ring's fragments: the first wait lets this wave's observation, bias and ring
@@ -1498,6 +1499,25 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (n0 + r < hot.head_n) o[n0 + r] = f4c(v, r);
+          }
+        }
+      });
+    } else if constexpr (CTL && PL) {
+      // the lean tick: the program's action epilogue is the identity (w4_plain) and the
+      // head's fields were read with the hot block, before the tile's observation rows
+      // went out. (dense_store read them here: vector loads queued behind those 6 KB of
+      // row stores, so the action stores waited for all of them.)
+      const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
+      with_act(hot.head_act, [&](auto act_k) {
+        constexpr int ACT = decltype(act_k)::value;
+        const float4 v = w4_epi<ACT>(ActP{hot.head_act, hot.head_alpha, hot.head_beta}, hs[0], hbv[0]);
+        if (row < B) {
+          if (hot.head_n == GO2PI_CTL_DOF) {
+            if (n0 < GO2PI_CTL_DOF) ctl_store4(cv, row, n0, {v.x, v.y, v.z, v.w});
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n0 + r < hot.head_n) ctl_store(cv, row, n0 + r, f4c(v, r));
           }
         }
       });
