@@ -1599,10 +1599,12 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
 // issued them ~2.7K cycles in, behind the chain kernel argument -> program -> its
 // fields (profiles/r05_clock_ctl.json, init_subphases.obs_issued). The rest of the
 // program and the controller arguments are read behind those loads.
-// shape = B | in_dim << 20 (B < 2^20, in_dim < 2^12: the engine checks).
+// shape = B | in_dim << 20 (B < 2^20, in_dim < 2^12: the engine checks). c0: layer 0's
+// k-chunk count (its K padded to 16 or to 64: not derivable from in_dim alone), needed
+// only after the staging, from the argument segment.
 template <int TPW, int HT, int C0M>
 __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &ctl, const float *l0w,
-                                            const float *bpack, unsigned shape, unsigned *yield) {
+                                            const float *bpack, unsigned shape, unsigned *yield, int c0) {
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   const int B = (int)(shape & 0xFFFFFu), in_dim = (int)(shape >> 20);
@@ -1626,8 +1628,7 @@ __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &c
   GO2PI_STAMP(P, tid == 0, 0);
   GO2PI_STAMP_RT(P, tid == 0, 1);
   GO2PI_STAMP(P, tid == 0, 41);
-  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, (in_dim + 15) >> 4, 0, 0,
-                          0.f, 0.f, 1, 0.f, 0.f, in_dim};
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f, in_dim};
   const CtlView cv = ctl_view(ctl, CL, row0);
   int ep = 0;
   float4 ring_none[4][TPW];  // (w4_step loads its own ring here)
@@ -2003,7 +2004,7 @@ __global__ __launch_bounds__(NW * 64) void policy_fused_ctl_kernel(const DevProg
 
 // The lean controller tick (w4_ctl_body). The first arguments, up to shape, are
 // preloaded into SGPRs (13 dwords); C (its row pointers repeat the preloaded ones),
-// Pd and yield come from the kernel argument segment, needed only later.
+// Pd, yield and c0 come from the kernel argument segment, needed only later.
 template <int TPW, int HT, int C0M>
 __global__ __launch_bounds__(256) void policy_mlp_ctl_kernel(const float *__restrict__ state,
                                                              const float *__restrict__ joy, float *__restrict__ obs,
@@ -2011,14 +2012,14 @@ __global__ __launch_bounds__(256) void policy_mlp_ctl_kernel(const float *__rest
                                                              const float *__restrict__ l0w, unsigned shape,
                                                              const float *__restrict__ bpack,
                                                              const DevProgram *__restrict__ Pd, unsigned *yield,
-                                                             DevCtl C) {
+                                                             int c0, DevCtl C) {
   DevCtl c = C;
   c.state = state;
   c.joy = joy;
   c.obs = obs;
   c.action = act;
   c.prm = prm;
-  w4_ctl_body<TPW, HT, C0M>(*Pd, c, l0w, bpack, shape, yield);
+  w4_ctl_body<TPW, HT, C0M>(*Pd, c, l0w, bpack, shape, yield, c0);
 }
 
 }  // namespace go2pi

@@ -176,6 +176,10 @@ MODELS = {
     "ctl_h1": lambda: mlp_model_bytes((49, 64, 64, 12), seed=7),
     "ctl_h3": lambda: mlp_model_bytes((147, 128, 128, 12), seed=8),
     "ctl_h16": lambda: mlp_model_bytes((784, 128, 128, 12), seed=17),  # the longest history (16 x 49)
+    # three hidden layers (the lean controller tick) at histories whose layer-0 K pads to 64
+    # (147 -> 10 chunks of 16, padded to 12; 196 -> 13, padded to 16)
+    "ctl_h3_deep": lambda: mlp_model_bytes((147, 128, 128, 128, 12), seed=9),
+    "ctl_h4_deep": lambda: mlp_model_bytes((196, 128, 128, 128, 12), seed=10),
     "gru_ctl": lambda: gru_model_bytes(I=98, H=64, head=(128, 12), seed=9),
     # shapes of the 4-wave pipeline (kernels.hip w4_step): tiles per wave x head tiles
     "pipe_256_h2": lambda: mlp_model_bytes((40, 256, 256, 20), seed=10),                      # 4 x 2, hand-off

@@ -69,12 +69,16 @@ def test_controller_long_closed_loop_no_joystick():
         _run_ticks(e, _mlp_policy(SHIPPED), 16, 50, seed=11, joy_mode="none")
 
 
-@pytest.mark.parametrize("name,hist", [("ctl_h1", 1), ("ctl_h3", 3), ("ctl_h16", 16)])
+@pytest.mark.parametrize("name,hist", [("ctl_h1", 1), ("ctl_h3", 3), ("ctl_h16", 16), ("ctl_h3_deep", 3),
+                                       ("ctl_h4_deep", 4)])
 @pytest.mark.parametrize("B,res", [(5, 0), (5, 500), (300, 0)])
 def test_controller_history_lengths(synth_path, name, hist, B, res):
     """Other history lengths (49 x kHistory observations): B = 5 by one launch per tick or
     by the resident kernel's controller form (the generic policy_act1_kernel shapes for
-    ctl_h1 and ctl_h3, the multi-workgroup form for ctl_h16), and the batched kernel."""
+    ctl_h1 and ctl_h3, the multi-workgroup form for ctl_h16), and the batched kernel.
+    The _deep variants (three hidden layers) take the lean tick kernel at B = 300 with a
+    layer 0 whose K pads to 64 (147 -> 192, 196 -> 256 columns): its chunk count is not
+    ceil(in_dim / 16)."""
     from go2_onnx_controller_amd import Engine
     p = synth_path(name)
     with Engine(p, max_batch=B, resident_ms=res) as e:
