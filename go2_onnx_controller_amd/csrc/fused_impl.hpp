@@ -1671,6 +1671,14 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   const DevGru G = P.gru;
   const float *w4_bpack = P.w4_bpack, *l0_w = P.l0_w;
   const int w4_bias = P.w4_bias;
+  // (clock builds: this workgroup's stamp row, read here too, so that the prologue's
+  // marks do not wait for the staging loads themselves)
+#ifdef GO2PI_DIAG_CLOCK
+  unsigned long long *srow = P.stamps ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr;
+#else
+  unsigned long long *srow = nullptr;
+#endif
+  (void)srow;
   // Touch every layer descriptor up front: one burst of scalar loads warms the
   // scalar cache, so each layer's start does not pay a K$ miss on its fields
   // (measured: layer entry ~990 -> ~740 cycles after the barrier).
@@ -1767,7 +1775,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   // next layer, so they must hold finite values: clear everything the
   // observation does not cover, once.
   stage_obs(0);
-  GO2PI_STAMP(P, tid == 0, 41);
+  GO2PI_STAMP_AT(srow, tid == 0, 41);
   if (zero_fill) {  // only a GRU whose H is not a multiple of 64 leaves such columns
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tail4 = (S - in_pad0) >> 2;
@@ -1801,7 +1809,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
       }
     }
   }
-  GO2PI_STAMP(P, tid == 0 && has_gru, 56);  // (GRU prologue marks: 56 hidden rows issued, 57 step loop, 58 cell entry)
+  GO2PI_STAMP_AT(srow, tid == 0 && has_gru, 56);  // (GRU prologue marks: 56 hidden rows issued, 57 step loop, 58 cell entry)
   // LSTM, pipeline: this lane's cell-state units (w4_lstm) in registers for the whole sequence
   float4 creg[4];
   if (RNN == 1 && W4T > 0 && has_gru && (H == 256 || H == 128)) {
@@ -1813,7 +1821,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   }
   for (int step = 0; step < steps; ++step) {
     float *ac = act + (size_t)step * B * out_dim;
-    GO2PI_STAMP(P, tid == 0 && step == 0 && has_gru, 57);
+    GO2PI_STAMP_AT(srow, tid == 0 && step == 0 && has_gru, 57);
     if (step > 0) stage_obs(step);
     if constexpr (W4T > 0) {  // the 4-wave uniform-MLP pipeline (its own barriers)
       static_assert(NW == 4, "one wave per SIMD");
@@ -1839,7 +1847,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
               w4_prefill<W4T, C0M>(l0_w, ring0, wave, lane);
             }
           };
-          GO2PI_STAMP(P, tid == 0 && step == 0, 58);
+          GO2PI_STAMP_AT(srow, tid == 0 && step == 0, 58);
           if constexpr (lstm) {
             float4 cr[GT];
 #pragma unroll
@@ -1849,7 +1857,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
             for (int i = 0; i < GT; ++i) creg[i] = cr[i];
           } else {
             w4_gru<GT>(G, bufA, bufH, bufB, S, wave, lane, hn,
-                       P.stamps && step == 0 ? P.stamps + blockIdx.x * GO2PI_STAMPS_PER_WG : nullptr, mid);
+                       step == 0 ? srow : nullptr, mid);
           }
           ring_pre = PREF;
           if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's state: once, from registers

@@ -24,3 +24,7 @@ if [ -f go2_onnx_controller_amd/lib/diag/libgo2pi_clock.so ]; then
 fi
 timeout -k 10 400 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || exit 1
 cat gpurun_out/bench_full.json
+# LSTM-256 lines (one tick per launch, 100 ticks per launch)
+timeout -k 10 200 python bench.py --workload go2_lstm_256_b4096 --no-cpu --no-latency --no-ctl --no-gru > gpurun_out/bench_lstm256.json 2> gpurun_out/bench_lstm256.err || exit 1
+timeout -k 10 200 python bench.py --workload go2_lstm_256_b4096_seq100 --no-cpu --no-latency --no-ctl --no-gru > gpurun_out/bench_lstm256_seq100.json 2> gpurun_out/bench_lstm256_seq100.err || exit 1
+echo lstm done
