@@ -35,6 +35,7 @@
 #include "onnx_model.hpp"
 #include "program.hpp"
 
+static bool gru_lean_on();
 namespace {
 
 thread_local std::string g_last_error;
@@ -1052,6 +1053,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
       p.w4_nw = (p.w4_tpw == 8 && p.w4_plain && p.w4_actc == 1 && p.w4_nhc == 3 && p.head_fuse <= 1 && w8 &&
                  w8[0] == '1') ? 8 : 4;
     }
+    // the lean GRU tick (policy_gru_kernel, r05): a GRU cell (lbr = 1, H = 128 or 256) in front of
+    // a dense chain the lean kernel would serve (gru_lean_on: GO2PI_GRU_LEAN / GO2PI_GRU_GENERAL)
+    p.w4_gru_lean = (p.has_gru && p.gru.cell == 0 && p.gru.lbr == 1 && (p.gru.H == 128 || p.gru.H == 256) &&
+                     p.gru.H <= 64 * p.w4_tpw && !p.pre_sub && !p.pre_div && !p.pre_mul && !p.pre_clip &&
+                     p.post_plain && p.lds_stride == 64 * p.w4_tpw + 4 && p.w4_actc == 1 && p.w4_nhc == 3 &&
+                     p.c0 == p.gru.H / 16 && p.gru.I_pad == (p.in_dim + 63) / 64 * 64 && p.in_dim < 4096 &&
+                     !p.zero_fill && gru_lean_on()) ? 1 : 0;
   }
   // a dense policy whose weights fit one CU's registers is served by the single-
   // workgroup resident kernel (no inter-workgroup hop per layer; GO2PI_RES_MULTI=1:
@@ -1639,13 +1647,22 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *c) {
   });
 }
 
+// the lean GRU tick by default? (GO2PI_GRU_LEAN=1 turns it on, GO2PI_GRU_GENERAL=1 off)
+static bool gru_lean_on() {
+  if (std::getenv("GO2PI_GRU_GENERAL")) return false;
+  const char *v = std::getenv("GO2PI_GRU_LEAN");
+  return v && v[0] == '1';
+}
+
 int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
   return guarded([&] {
     check_engine(e);
     if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
     const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
     const int c0m = t ? e->prog.w4_c0m : 0;
-    if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
+    if (t && e->prog.w4_gru_lean)  // the lean GRU tick: <tiles per wave, head tiles, hidden tiles per wave>
+      std::snprintf(buf, cap, "policy_gru_kernel<%d, %d, %d>", t, h, e->prog.gru.H / 64);
+    else if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
                                 // act, hidden layers>
       // (<..., waves per workgroup>: 4, or 8 with half the tiles per wave)
       if (e->prog.w4_nw == 8)

@@ -1638,6 +1638,96 @@ __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &c
   GO2PI_STAMP_RT(P, tid == 0, 3);
 }
 
+// The lean GRU tick (r05): a GRU cell (lbr = 1, H = 64 GT) in
+// front of a dense chain the lean kernel serves (Elu, three hidden layers 64 TPW wide, no
+// prologue or epilogue arithmetic). The general body's prologue was instruction-bound:
+// ~1.2K scalar and spill instructions of run-time shape arithmetic between the
+// observation's loads, the hidden rows' loads and the cell (clock marks 41 / 56 / 57:
+// 1.7K, 3.8K, 6.2K cycles, profiles/r05_clock_gru256.json). Here the shape is compile
+// time (H, the LDS stride, the bias pack), and the observation, hidden state, cell
+// weights, dense arena, bias pack and B | in_dim << 20 are the preloaded kernel
+// arguments, so the observation rows, the hidden rows (16-byte direct-to-LDS loads: one
+// per 256 units of a row) and the cell's first fragments go out at once. Gate biases,
+// the program and yield come from the argument segment.
+template <int TPW, int HT, int GT>
+__device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *obs, float *act, float *hidden,
+                                            const float *gw, const float *l0w, const float *bpack, unsigned shape,
+                                            const float *gbzr, const float *gbh, int steps, unsigned *yield) {
+  extern __shared__ float4 lds4[];
+  float *lds = reinterpret_cast<float *>(lds4);
+  constexpr int H = 64 * GT, S = 64 * TPW + 4, NBIAS = 3 * 64 * TPW;
+  static_assert(H <= 64 * TPW, "the hidden rows fit the LDS row");
+  const int B = (int)(shape & 0xFFFFFu), in_dim = (int)(shape >> 20);
+  const int ipad = (in_dim + 63) & ~63, nch = ipad >> 6;  // (pack_gru: x padded to whole 64-column groups)
+  float *bufA = lds, *bufB = lds + GO2PI_TILE_ROWS * S, *bufH = lds + 2 * GO2PI_TILE_ROWS * S;
+  f32x4 *scratch = reinterpret_cast<f32x4 *>(lds + 3 * GO2PI_TILE_ROWS * S);
+  int *flags = reinterpret_cast<int *>(lds + 3 * GO2PI_TILE_ROWS * S + 256 * 4 * HT);
+  float *lbias = reinterpret_cast<float *>(flags) + GO2PI_FLAG_FLOATS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = blockIdx.x * GO2PI_TILE_ROWS;
+  // wave w stages rows w, w + 4, w + 8, w + 12; padding lanes read an element of the same
+  // row (times a zero weight column), rows past B the last row (their results are dropped)
+  auto stage_obs = [&](int step) {
+    const float *ob = obs + (size_t)step * B * in_dim;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wave + 4 * i;
+      const float *rp = ob + (size_t)min(row0 + r, B - 1) * in_dim;
+      for (int c = 0; c < nch; ++c)
+        __builtin_amdgcn_global_load_lds((gvoid_t *)(rp + min(c * 64 + lane, in_dim - 1)),
+                                         (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
+    }
+  };
+  stage_obs(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wave + 4 * i;
+    const float *hp = hidden + (size_t)min(row0 + r, B - 1) * H;
+    if constexpr (H % 256 == 0) {
+#pragma unroll
+      for (int c = 0; c < H / 256; ++c)
+        __builtin_amdgcn_global_load_lds((gvoid_t *)(hp + c * 256 + 4 * lane), (lvoid_t *)(bufH + r * S + c * 256),
+                                         16, 0, 0);
+    } else {
+#pragma unroll
+      for (int c = 0; c < H / 64; ++c)
+        __builtin_amdgcn_global_load_lds((gvoid_t *)(hp + c * 64 + lane), (lvoid_t *)(bufH + r * S + c * 64), 4, 0, 0);
+    }
+  }
+  // the dense chain's biases too: the cell's staging barrier (vmcnt behind its first
+  // fragments) then covers them, so no later wait counts on the ring's loads being younger
+  glds_copy(lbias, bpack, NBIAS, wave, lane, 4);
+  if (tid < 4) flags[tid] = 0;
+  if (blockIdx.x == 0 && tid == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
+    __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  GO2PI_STAMP(P, tid == 0, 0);
+  GO2PI_STAMP_RT(P, tid == 0, 1);
+  const DevGru G{gw, gbzr, gbh, in_dim, ipad, H, 1, 0, H};
+  const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, H / 16, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
+  int ep = 0;
+  for (int step = 0; step < steps; ++step) {
+    if (step > 0) stage_obs(step);
+    float4 ring0[4][TPW];  // the dense chain's layer-0 ring, filled behind the cell (w4_prefill)
+    float4 hn[GT];
+    auto mid = [&] { w4_prefill<TPW, 0>(l0w, ring0, wave, lane); };
+    w4_gru<GT>(G, bufA, bufH, bufB, S, wave, lane, hn, nullptr, mid);
+    if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's state: once, from registers
+      float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+      for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + i * 16) = hn[i];
+    }
+    lds_barrier();  // every wave has read bufH (an LDS hand-off: no wait for the ring's loads)
+    float *hl = bufH + (lane & 15) * S + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+    for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hl + i * 16) = hn[i];
+    w4_step<TPW, HT, false, true, 0, 1, 3>(P, hot, bufB, bufA, S, scratch, flags, lbias, ep, wave, lane, act,
+                                           CtlView{}, row0, B, DevCtl{}, CtlLds{}, step, ring0, true);
+  }
+  GO2PI_STAMP(P, tid == 0, 2);
+  GO2PI_STAMP_RT(P, tid == 0, 3);
+}
+
 // RNN: the recurrent cell this instantiation runs when the program has one (0 GRU,
 // 1 LSTM; one kernel per cell keeps the other cell's registers out of it).
 template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0, int ACTC = -1, int NHC = 0>
@@ -2002,6 +2092,19 @@ __global__ __launch_bounds__(NW * 64) void policy_mlp_kernel(const float *__rest
                                                              const DevProgram *__restrict__ Pd, int B, int steps,
                                                              unsigned dims, unsigned *yield) {
   w4_plain_body<TPW, HT, C0M, ACTC, NHC, NW>(*Pd, obs, act, l0w, bpack, B, steps, dims, yield);
+}
+
+// The lean GRU tick (w4_gru_body): the arguments up to shape are preloaded into SGPRs
+// (13 dwords); the rest come from the argument segment.
+template <int TPW, int HT, int GT>
+__global__ __launch_bounds__(256) void policy_gru_kernel(const float *__restrict__ obs, float *__restrict__ act,
+                                                         float *__restrict__ hidden, const float *__restrict__ gw,
+                                                         const float *__restrict__ l0w,
+                                                         const float *__restrict__ bpack, unsigned shape,
+                                                         const float *gbzr, const float *gbh,
+                                                         const DevProgram *__restrict__ Pd, int steps,
+                                                         unsigned *yield) {
+  w4_gru_body<TPW, HT, GT>(*Pd, obs, act, hidden, gw, l0w, bpack, shape, gbzr, gbh, steps, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>

@@ -50,14 +50,16 @@ def test_pipeline_shapes(synth_path, name):
             assert abs_err(gen.run(x[:B]), want) <= TOL, (name, B)
 
 
-@pytest.mark.parametrize("name,kernel,env", [("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, 1, 3>", {}),
+@pytest.mark.parametrize("name,kernel,env", [("go2_gru_256", "policy_gru_kernel<8, 1, 4>", {"GO2PI_GRU_LEAN": "1"}),
+                                             ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, 1, 3>", {}),
                                              ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, -1, 0>",
                                               {"GO2PI_LEAN_RT_NH": "1"}),
                                              ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0, -1, 0>", {})])
 def test_pipeline_gru_ticks(synth_path, monkeypatch, name, kernel, env):
     """GRU front stage + MLP pipeline over several ticks (hidden state carried by
     the engine), against the fp64 ONNX GRU oracle, actions and hidden state; the
-    dense layers with the compile-time Elu and layer count, and the runtime forms."""
+    lean GRU tick (policy_gru_kernel), the general body with the compile-time Elu and
+    layer count, and the runtime forms."""
     from go2_onnx_controller_amd import Engine
     from oracle import onnx_ref
     for k, v in env.items():
