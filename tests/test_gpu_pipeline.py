@@ -50,8 +50,9 @@ def test_pipeline_shapes(synth_path, name):
             assert abs_err(gen.run(x[:B]), want) <= TOL, (name, B)
 
 
-@pytest.mark.parametrize("name,kernel,env", [("go2_gru_256", "policy_gru_kernel<8, 1, 4>", {"GO2PI_GRU_LEAN": "1"}),
-                                             ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, 1, 3>", {}),
+@pytest.mark.parametrize("name,kernel,env", [("go2_gru_256", "policy_gru_kernel<8, 1, 4>", {}),
+                                             ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, 1, 3>",
+                                              {"GO2PI_GRU_GENERAL": "1"}),
                                              ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, -1, 0>",
                                               {"GO2PI_LEAN_RT_NH": "1"}),
                                              ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0, -1, 0>", {})])
