@@ -1055,8 +1055,7 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     }
     // the lean GRU tick (policy_gru_kernel, r05): a GRU cell (lbr = 1) in front of
     // a dense chain the lean kernel would serve (gru_lean_on: GO2PI_GRU_LEAN / GO2PI_GRU_GENERAL)
-    // (H = 256 only: the GT = 2 instantiation, H = 128, is built but not yet measured or tested)
-    p.w4_gru_lean = (p.has_gru && p.gru.cell == 0 && p.gru.lbr == 1 && p.gru.H == 256 &&
+    p.w4_gru_lean = (p.has_gru && p.gru.cell == 0 && p.gru.lbr == 1 && (p.gru.H == 128 || p.gru.H == 256) &&
                      p.gru.H <= 64 * p.w4_tpw && !p.pre_sub && !p.pre_div && !p.pre_mul && !p.pre_clip &&
                      p.post_plain && p.lds_stride == 64 * p.w4_tpw + 4 && p.w4_actc == 1 && p.w4_nhc == 3 &&
                      p.c0 == p.gru.H / 16 && p.gru.I_pad == (p.in_dim + 63) / 64 * 64 && p.in_dim < 4096 &&

@@ -187,6 +187,7 @@ MODELS = {
     "pipe_512_relu": lambda: mlp_model_bytes((70, 512, 512, 7), seed=12, act="Relu"),         # 8 x 1, K0 = 128
     "pipe_one_hidden": lambda: mlp_model_bytes((48, 256, 12), seed=13),                       # one hidden layer
     "gru_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=14),            # 2-tile GRU stage
+    "gru_128_deep": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 256, 12), seed=15),  # lean GRU tick, H = 128
     # GRU with linear_before_reset = 0 (the attribute left at its ONNX default): the
     # generic body's two-pass cell (fused_impl.hpp gru0_cell)
     "gru_lbr0_small": lambda: gru_model_bytes(I=10, H=32, head=(64, 6), seed=18, lbr=0),

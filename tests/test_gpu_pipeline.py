@@ -55,7 +55,10 @@ def test_pipeline_shapes(synth_path, name):
                                               {"GO2PI_GRU_GENERAL": "1"}),
                                              ("go2_gru_256", "policy_fused_kernel<4, 8, 1, 0, 0, -1, 0>",
                                               {"GO2PI_LEAN_RT_NH": "1"}),
-                                             ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0, -1, 0>", {})])
+                                             ("gru_128", "policy_fused_kernel<4, 4, 1, 0, 0, -1, 0>", {}),
+                                             ("gru_128_deep", "policy_gru_kernel<4, 1, 2>", {}),
+                                             ("gru_128_deep", "policy_fused_kernel<4, 4, 1, 0, 0, 1, 3>",
+                                              {"GO2PI_GRU_GENERAL": "1"})])
 def test_pipeline_gru_ticks(synth_path, monkeypatch, name, kernel, env):
     """GRU front stage + MLP pipeline over several ticks (hidden state carried by
     the engine), against the fp64 ONNX GRU oracle, actions and hidden state; the
