@@ -105,10 +105,29 @@ void pin_give(void *p, size_t bytes) {
 std::vector<std::tuple<int, size_t, void *>> g_bar_free;  // (device, bytes, block), under g_pin_mu
 std::vector<int> g_bar_absent;                            // devices whose VRAM the host cannot map
 
+// true when [p, p + bytes) lies inside mappings of this process that are readable
+// and writable from the CPU. ROCm's thunk reserves the GPU's virtual aperture with
+// PROT_NONE mappings, so an address range being mapped (msync succeeds) does not make
+// it host-accessible: without large BAR a fine-grained VRAM block sits in such a range
+// and a host store to it faults. /proc/self/maps gives the protection.
 bool host_mapped(const void *p, size_t bytes) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
-  const size_t n = ((reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095)) - a;
-  return msync(reinterpret_cast<void *>(a), n, MS_ASYNC) == 0;
+  uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uintptr_t end = a + bytes;
+  FILE *f = std::fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  char line[512];
+  bool ok = false;
+  while (a < end && std::fgets(line, sizeof line, f)) {  // (ascending address order)
+    unsigned long lo = 0, hi = 0;
+    char perm[8] = {0};
+    if (std::sscanf(line, "%lx-%lx %7s", &lo, &hi, perm) != 3) continue;
+    if (hi <= a) continue;
+    if (lo > a || perm[0] != 'r' || perm[1] != 'w') break;  // a hole, or not read-write
+    a = hi;  // covered up to hi; the rest must follow in the next mapping(s)
+  }
+  ok = a >= end;
+  std::fclose(f);
+  return ok;
 }
 
 // a host-writable device block of at least `bytes` (out: its size) on the current
@@ -131,12 +150,12 @@ void *bar_take(int device, size_t &bytes) {
   if (!p) {
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
       (void)hipGetLastError();
-      p = nullptr;
+      return nullptr;  // (this engine only: an allocation failure may be transient)
     }
-    if (!p || !host_mapped(p, bytes)) {
+    if (!host_mapped(p, bytes)) {  // the host cannot map this device's memory: for the whole process
       std::lock_guard<std::mutex> lk(g_pin_mu);
       g_bar_absent.push_back(device);
-      if (p) g_bar_free.emplace_back(device, bytes, p);  // (kept: hipFree would synchronise the device)
+      g_bar_free.emplace_back(device, bytes, p);  // (kept: hipFree would synchronise the device)
       return nullptr;
     }
   }
@@ -213,6 +232,7 @@ struct go2pi_engine {
   bool resident_ctl = false;  // the live kernel is the controller-tick form
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
+  bool wide = false;          // act() form for wide policies (resident_wide.hip policy_wide_kernel, r06)
   bool ctl_gran_ok = false;   // ... answered in granules (policy_act1_kernel, r05): no done word per tick
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // request granules: host view, device view
@@ -339,6 +359,10 @@ struct go2pi_engine {
       hip_check(go2pi::launch_resident1(prog, d_prog, m_req, m_actg, m_err, m_done, res_idle_ticks, prog.yield, ctl,
                                         stream),
                 "resident launch (one workgroup)");
+    else if (!ctl && wide)
+      hip_check(go2pi::launch_resident_wide(prog, d_prog, m_req, m_actg, d_gran, gstride, m_err, m_done, res_idle_ticks,
+                                            prog.yield, stream),
+                "resident launch (wide policy)");
     else
       hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,
                                        res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
@@ -1067,6 +1091,13 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, false) && !std::getenv("GO2PI_RES_MULTI");
   e.resident1_ctl = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, true) && !std::getenv("GO2PI_RES_MULTI");
   e.ctl_gran_ok = e.resident1_ctl && go2pi::resident1_ctl_granules(p);
+  // a wide dense policy (every hidden layer 256 or 512 wide: BASELINE configs[1]'s
+  // 48 -> 512^3 -> 12) is served by policy_wide_kernel when every workgroup can poll the
+  // request ring in device memory (large BAR); else by the multi-workgroup kernel, whose
+  // workgroup 0 alone polls the host and mirrors the request (GO2PI_RES_MULTI=1: that
+  // form regardless, A/B and its tests)
+  e.wide = e.resident_ok && !e.resident1 && !m.has_gru && e.req_bar_bytes > 0 && go2pi::wide_shape(p).nl > 0 &&
+           !std::getenv("GO2PI_RES_MULTI");
   hip_check(go2pi::configure_kernels(p, e.waves), "hipFuncSetAttribute");
   e.d_prog = e.dalloc<go2pi::DevProgram>(1);
   hip_check(hipMemcpy(e.d_prog, &p, sizeof(p), hipMemcpyHostToDevice), "hipMemcpy");
@@ -1236,7 +1267,12 @@ int go2pi_io_dims(const go2pi_engine *e, int64_t *in_dim, int64_t *out_dim) {
 
 int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
   // batch <= 8 on a live resident kernel: served with no HIP runtime call (the device
-  // switch and its restore were three HIP API entries per act(), on the 5 us path)
+  // switch and its restore were three HIP API entries per act(), on the 5 us path).
+  // Invariant: this skips check_engine / check_batch because a live kernel
+  // (resident_ready: resident_live) exists only after an earlier call on this engine
+  // passed them in the guarded path below (resident_start is reached from there only),
+  // and the fields read here (opts, resident_ok, model dims) never change after build.
+  // The batch bounds are re-checked in the condition itself.
   bool res_try = true;
   if (e && obs && act && batch >= 1 && batch <= GO2PI_SMALL_MAXB && batch <= e->opts.max_batch && e->resident_ok &&
       e->resident_ready(nullptr)) {
@@ -1462,7 +1498,11 @@ void check_ctl(const go2pi_engine *e, int64_t batch) {
 int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy, float *obs, float *action,
                           double *q_des, double *kp, double *kd, uint32_t *status, int64_t batch) {
   // batch <= 8 on a live controller-form resident kernel: no HIP runtime call and no
-  // input staging (the rows travel in the request itself; go2pi_run's fast path)
+  // input staging (the rows travel in the request itself; go2pi_run's fast path).
+  // Invariant: check_ctl is skipped; the condition itself requires ctl_hist
+  // (a controller policy: check_ctl's model test), the batch bounds and the staging
+  // (h_ctl), and resident_ready(&all) requires a live controller-form kernel, which only
+  // the guarded path below starts.
   bool res_try = true;
   if (e && state && obs && action && batch >= 1 && batch <= GO2PI_SMALL_MAXB && batch <= e->opts.max_batch &&
       e->ctl_hist && e->resident_ok && e->resident_ctl_ok && e->done_ok && e->h_ctl) {
@@ -1670,6 +1710,27 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0, t ? e->prog.w4_actc : -1,
                     t ? e->prog.w4_nhc : 0);
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_resident_kernel(const go2pi_engine *e, char *buf, size_t cap) {
+  return guarded([&] {
+    check_engine(e);
+    if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
+    const char *ring = e->req_bar_bytes ? " ring=vram" : " ring=host";
+    if (!e->resident_ok) {
+      std::snprintf(buf, cap, "none");
+    } else if (e->resident1) {
+      std::snprintf(buf, cap, "%s%s",
+                    go2pi::resident1_ctl_granules(e->prog) ? "policy_act1_kernel" : "policy_resident1_kernel", ring);
+    } else if (e->wide) {
+      const go2pi::WideShape w = go2pi::wide_shape(e->prog);
+      const bool pro = e->prog.pre_sub || e->prog.pre_div || e->prog.pre_mul || e->prog.pre_clip;
+      std::snprintf(buf, cap, "policy_wide_kernel<%d, %d, %d, %d>%s", w.nl, w.cw, w.f0, pro ? 1 : 0, ring);
+    } else {
+      std::snprintf(buf, cap, "policy_resident_kernel%s", ring);
+    }
     return GO2PI_OK;
   });
 }

@@ -339,7 +339,9 @@ void front_end(Model &m, const std::vector<Node> &nodes, const std::unordered_ma
     const std::string &o = nd.in.at(0) == x ? nd.in.at(1) : nd.in.at(0);
     auto it = inits.find(o);
     if (it == inits.end() || it->second.dtype != 1) fail(nd.op + " in the observation front-end needs a FLOAT constant");
-    if (nd.op == "Div" && nd.in.at(0) != x) fail("Div in the observation front-end must divide the observation");
+    // (a constant first would be c / x or c - x: lowered as x / c or x - c, the wrong value)
+    if ((nd.op == "Div" || nd.op == "Sub") && nd.in.at(0) != x)
+      fail(nd.op + " in the observation front-end must take the observation as its first input");
     return it->second;
   };
   struct Block {

@@ -255,4 +255,18 @@ int launch_resident1(const DevProgram &p, const DevProgram *p_dev, const unsigne
                      unsigned long long *actg, unsigned *err, unsigned *done, unsigned long long idle_ticks,
                      const unsigned *yield, const DevCtl *ctl, void *stream);
 
+// The resident act() for wide dense policies (resident_wide.hip policy_wide_kernel, r06):
+// 3..5 dense layers, every hidden layer H = 256 or 512 wide, a head of <= 16 outputs,
+// layer 0 of K_pad <= 64. H / 16 workgroups, each polling the request ring itself (the
+// ring must be in device memory: the host writes it through the large-BAR mapping).
+// Same request / answer / leave protocol as launch_resident1 (act() form only); gran:
+// [nl - 1][gstride >= 8 H] granules, zeroed before every launch.
+struct WideShape {
+  int nl, cw, f0;
+};
+WideShape wide_shape(const DevProgram &p);  // nl = 0: does not apply
+int launch_resident_wide(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,
+                         unsigned long long *actg, unsigned long long *gran, int gstride, unsigned *err, unsigned *done,
+                         unsigned long long idle_ticks, const unsigned *yield, void *stream);
+
 }  // namespace go2pi

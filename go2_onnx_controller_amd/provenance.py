@@ -14,11 +14,15 @@ CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
 
 
 def kernel_source_digest() -> str:
-    """sha256 (first 16 hex) over every device-code source and the build flags:
-    csrc/*.hip, *.hpp, *.inc and the Makefile, in name order."""
+    """sha256 (first 16 hex) over every source that decides what the device runs and
+    the build flags: csrc/*.hip, *.hpp, *.inc (the kernels), engine.cpp and
+    onnx_model.cpp (weight packing and padding, kernel choice and launch shapes: a
+    packing change moves the traffic as surely as a kernel change) and the
+    Makefile, in name order."""
     h = hashlib.sha256()
     files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.hpp")) +
-                   glob.glob(os.path.join(CSRC, "*.inc")) + [os.path.join(CSRC, "Makefile")])
+                   glob.glob(os.path.join(CSRC, "*.inc")) + glob.glob(os.path.join(CSRC, "*.cpp")) +
+                   [os.path.join(CSRC, "Makefile")])
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:

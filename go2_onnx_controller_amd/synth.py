@@ -186,6 +186,11 @@ MODELS = {
     "pipe_128_tanh_h2": lambda: mlp_model_bytes((33, 128, 128, 128, 30), seed=11, act="Tanh"),  # 2 x 2, barrier
     "pipe_512_relu": lambda: mlp_model_bytes((70, 512, 512, 7), seed=12, act="Relu"),         # 8 x 1, K0 = 128
     "pipe_one_hidden": lambda: mlp_model_bytes((48, 256, 12), seed=13),                       # one hidden layer
+    # the resident wide-policy kernel's other shapes (resident_wide.hip): hidden width 256
+    # (four compute waves) with one and two sliced layers, 512 with one; a 16-output head
+    "wide_256_3": lambda: mlp_model_bytes((45, 256, 256, 16), seed=21),
+    "wide_256_4": lambda: mlp_model_bytes((60, 256, 256, 256, 12), seed=22, act="Tanh"),
+    "wide_512_3": lambda: mlp_model_bytes((33, 512, 512, 10), seed=23, act="Relu"),
     "gru_128": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 12), seed=14),            # 2-tile GRU stage
     "gru_128_deep": lambda: gru_model_bytes(I=30, H=128, head=(256, 256, 256, 12), seed=15),  # lean GRU tick, H = 128
     # GRU with linear_before_reset = 0 (the attribute left at its ONNX default): the

@@ -133,6 +133,14 @@ int go2pi_get_cost(const go2pi_engine *e, go2pi_cost *cost);
    profiling tools; no compute. */
 int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap);
 
+/* Name of the resident kernel that serves go2pi_run at batch <= 8 on this engine
+   (opts.resident_ms > 0), then " ring=vram" when the request ring is in device
+   memory the host writes through the large-BAR mapping, " ring=host" when it is in
+   pinned host memory; "none" when no resident kernel serves act(). E.g.
+   "policy_wide_kernel<4, 8, 12, 0> ring=vram". For tests and profiling tools; no
+   compute. */
+int go2pi_resident_kernel(const go2pi_engine *e, char *buf, size_t cap);
+
 /* Parse and lower an ONNX policy WITHOUT touching a device (no compute): writes a
    JSON description (I/O names and shapes, the lowered layer program with
    per-layer weight/bias checksums) into buf. Returns the JSON length (>= 0) or an

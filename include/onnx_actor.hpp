@@ -5,7 +5,7 @@
  * constructor signature, default argument, act(), print_model_info() and
  * check_dims(), so `onnx_controller` (controller.cpp:25,49,215) compiles
  * unchanged, and so does the demo driver's use of the actor and of the Ort
- * namespace (src/cpp/main.cpp:26-45; tests/cpp/main_shape.cpp). The rest of
+ * namespace (src/cpp/main.cpp:26-45; tests/cpp/controller_shape.cpp). The rest of
  * main.cpp is not ours to provide: its model path comes from ROS's
  * ament_index_cpp (:29), and its `std::cout << duration` (:42) needs a C++20
  * standard library with P0355's chrono output (libstdc++ >= 14).

@@ -200,11 +200,14 @@ UNSUPPORTED = {
     # of order (a column permutation), and blocks clipped to different intervals
     "slice_reordered": lambda: _front([(4, 8), (0, 4)], clips=None),
     "slice_clip_differs": lambda: _front([(0, 4), (4, 8)], clips=[(-1.0, 1.0), (-2.0, 2.0)]),
+    # a block computing mean - x (the constant first): not the prologue's x - sub
+    "slice_sub_reversed": lambda: _front([(0, 4), (4, 8)], clips=None, sub_first=True),
 }
 
 
-def _front(blocks, clips):
-    """obs[8] -> Slice blocks (-> Clip) -> Concat -> Gemm -> act[3] (refusal cases)."""
+def _front(blocks, clips, sub_first=False):
+    """obs[8] -> Slice blocks (-> Clip) -> Concat -> Gemm -> act[3] (refusal cases);
+    sub_first: block 0 goes through Sub(constant, block) first."""
     r = _rng(6)
     inits = [("W", r.standard_normal((3, 8)).astype(np.float32)), ("ax", np.array([1], np.int64))]
     nodes, outs = [], []
@@ -212,6 +215,10 @@ def _front(blocks, clips):
         inits += [(f"s{i}", np.array([b], np.int64)), (f"e{i}", np.array([e], np.int64))]
         nodes.append(ow.node("Slice", ["obs", f"s{i}", f"e{i}", "ax"], [f"b{i}"]))
         out = f"b{i}"
+        if sub_first and i == 0:
+            inits.append(("m0", r.standard_normal(e - b).astype(np.float32)))
+            nodes.append(ow.node("Sub", ["m0", out], ["d0"]))
+            out = "d0"
         if clips:
             inits += [(f"lo{i}", np.array(clips[i][0], np.float32)), (f"hi{i}", np.array(clips[i][1], np.float32))]
             nodes.append(ow.node("Clip", [out, f"lo{i}", f"hi{i}"], [f"c{i}"]))

@@ -131,7 +131,9 @@ def test_loader_graph_variants(tmp_path, kind):
                                       ("mul_then_clip_out", "Clip after a Mul"),
                                       ("vector_mul_out", "per-feature Mul after the final activation"),
                                       ("slice_reordered", "cover its columns in order"),
-                                      ("slice_clip_differs", "Clip bounds differ")])
+                                      ("slice_clip_differs", "Clip bounds differ"),
+                                      ("slice_sub_reversed", "Sub in the observation front-end must take the "
+                                                             "observation as its first input")])
 def test_loader_rejects_unsupported(tmp_path, kind, msg):
     from go2_onnx_controller_amd import engine
     with pytest.raises(engine.Go2piError, match=msg):

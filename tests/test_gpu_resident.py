@@ -22,7 +22,8 @@ TOL = 1e-5
 
 
 def _models(synth_path):
-    return {"shipped": SHIPPED, "mlp512": synth_path("go2_mlp_512")}
+    return {"shipped": SHIPPED, "mlp512": synth_path("go2_mlp_512"), "wide_256_3": synth_path("wide_256_3"),
+            "wide_256_4": synth_path("wide_256_4"), "wide_512_3": synth_path("wide_512_3")}
 
 
 # resident forms: "one" the single-workgroup kernel (the default where the weights fit
@@ -30,12 +31,17 @@ def _models(synth_path):
 # two poll sweeps in flight), "one_d1" the same with one sweep in flight, "one_c4" with
 # four compute waves instead of eight, "one_r1w" the
 # r04 1024-thread form (GO2PI_RES_R1W=1), "multi" the multi-workgroup kernel
-# (GO2PI_RES_MULTI=1 for the shipped model; the only form for mlp512), "tiled0" multi
-# with layer 0 tiled like every other layer (bit-identical to the launch path)
+# (GO2PI_RES_MULTI=1; for mlp512 the form without large BAR), "tiled0" multi with
+# layer 0 tiled like every other layer (bit-identical to the launch path), "wide" the
+# wide-policy kernel (r06 policy_wide_kernel, the default for 256- and 512-wide policies
+# where the request ring is in device memory): mlp512 (BASELINE configs[1]), hidden width
+# 256 with one and two sliced layers, 512 with one
 @pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "one_d1"), ("shipped", "one_c4"),
                                        ("shipped", "one_r1w"),
                                        ("shipped", "multi"), ("shipped", "tiled0"),
-                                       ("mlp512", "multi"), ("mlp512", "tiled0")])
+                                       ("mlp512", "multi"), ("mlp512", "tiled0"),
+                                       ("mlp512", "wide"), ("wide_256_3", "wide"), ("wide_256_4", "wide"),
+                                       ("wide_512_3", "wide")])
 def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
     from go2_onnx_controller_amd import Engine
     from oracle import mlp_ref
@@ -46,13 +52,18 @@ def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
         monkeypatch.setenv("GO2PI_A1_CW", "4")  # four compute waves (one per SIMD)
     elif form == "one_r1w":
         monkeypatch.setenv("GO2PI_RES_R1W", "1")
-    elif form != "one":
+    elif form not in ("one", "wide"):
         monkeypatch.setenv("GO2PI_RES_MULTI", "1")  # read at engine creation
     if tiled0:
         monkeypatch.setenv("GO2PI_RES_TILED0", "1")  # read at each resident launch
     path = _models(synth_path)[name]
     ref = mlp_ref.MlpRef.from_onnx(path)
     with Engine(path, max_batch=64, resident_ms=500) as r, Engine(path, max_batch=64) as p:
+        if form == "wide":  # (without large BAR the multi-workgroup kernel serves, ring in host memory)
+            want = "policy_wide_kernel" if r.resident_kernel.endswith("ring=vram") else "policy_resident_kernel"
+            assert r.resident_kernel.startswith(want), r.resident_kernel
+        elif form == "multi" or tiled0:
+            assert r.resident_kernel.startswith("policy_resident_kernel"), r.resident_kernel
         rng = np.random.default_rng(7)
         for i, B in enumerate([1, 1, 2, 3, 1, 8, 5, 1, 4, 1] * 3):
             x = (realistic_obs(B, seed=i) if name == "shipped"
@@ -78,6 +89,56 @@ def test_resident_known_answers():
         for _ in range(3):
             for name in ("zeros", "twos"):
                 assert rel_err(e.run(g[f"{name}_x"]), g[f"{name}_y"]) <= TOL, name
+
+
+def test_resident_wide_known_answers(synth_path):
+    """The wide-policy kernel on the committed mlp512 fixture (tests/golden/golden_mlp512.npz,
+    fp64 ONNX oracle outputs), row by row at batch 1 and all rows at batch 8, over
+    repeated requests; the answer is deterministic across requests."""
+    import os
+    from conftest import GOLDEN
+    from go2_onnx_controller_amd import Engine
+    g = np.load(os.path.join(GOLDEN, "golden_mlp512.npz"))
+    x, want = g["x"].astype(np.float32), g["y"]
+    with Engine(synth_path("go2_mlp_512"), max_batch=8, resident_ms=500) as e:
+        first = None
+        for rep in range(3):
+            for i in range(min(len(x), 8)):
+                assert abs_err(e.run(x[i:i + 1]), want[i:i + 1]) <= TOL, f"rep {rep} row {i}"
+            y8 = e.run(x[:8])
+            assert abs_err(y8, want[:8]) <= TOL
+            first = y8 if first is None else first
+            assert np.array_equal(y8, first), "the resident answer changed between requests"
+
+
+@pytest.mark.parametrize("name", ["shipped", "mlp512"])
+def test_resident_request_ring_in_host_memory(synth_path, name, monkeypatch):
+    """GO2PI_REQ_HOST=1: the request ring in pinned host memory, as on a host without
+    large BAR (the production path there; engine.cpp bar_take falls back to it). act() at
+    batch 1 and 8 and the controller tick at batch 1 and 8 (shipped model) against the
+    fp64 oracle."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import controller_ref as cr
+    from oracle import mlp_ref
+    monkeypatch.setenv("GO2PI_REQ_HOST", "1")  # read at engine creation
+    path = _models(synth_path)[name]
+    ref = mlp_ref.MlpRef.from_onnx(path)
+    rng = np.random.default_rng(37)
+    with Engine(path, max_batch=8, resident_ms=500) as e:
+        assert e.resident_kernel.endswith("ring=host"), e.resident_kernel
+        for i, B in enumerate([1, 8, 1, 3, 8, 1] * 3):
+            x = realistic_obs(B, seed=200 + i) if name == "shipped" else rng.standard_normal((B, 48)).astype(np.float32)
+            assert abs_err(e.run(x), ref.f64(x)) <= TOL, f"call {i} B={B}"
+        if name == "shipped":
+            for i, B in enumerate([1, 8, 1, 8]):
+                st, joy = cr.synthetic_states(rng, B), cr.synthetic_joy(rng, B)
+                obs = rng.standard_normal((B, 98)).astype(np.float32)
+                act = rng.standard_normal((B, 12)).astype(np.float32)
+                want_obs, _ = cr.assemble_obs(obs, act, st, joy, 2)
+                a_ref = cr.post_process(ref.f64(want_obs), joy)[0]
+                e.controller_step(st, obs, act, joy=joy)
+                assert np.array_equal(obs, want_obs), f"tick {i}: observation differs"
+                assert rel_err(act, a_ref) <= TOL, f"tick {i}"
 
 
 def test_resident_interleaved_with_batched_calls(synth_path):

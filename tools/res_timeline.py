@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "res_timeline.json"))
     ap.add_argument("--ctl", action="store_true",
                     help="time the controller tick (go2pi_controller_step, batch 1) instead of act()")
-    ap.add_argument("--form", choices=["multi", "one"], default="multi",
+    ap.add_argument("--form", choices=["multi", "one", "wide"], default="multi",
                     help="the resident kernel the engine runs: multi-workgroup (policy_resident_kernel) or the "
                          "single-workgroup policy_resident1_kernel (r04; GO2PI_RES_MULTI=1 forces multi)")
     args = ap.parse_args()
@@ -69,6 +69,8 @@ def main():
     ts.sort()
     if args.form == "one":
         return one_workgroup(args, st, ts, np)
+    if args.form == "wide":
+        return wide(args, st, ts, np, e.resident_kernel)
     rows = st[(st[:, 0] > 0) & (st[:, 9] > 0)]
     base = rows[:, 0:1]
     rel = (rows - base) * 10.0 / 1e3  # us
@@ -144,6 +146,35 @@ def one_workgroup(args, st, ts, np):
            "wave0_cycles_since_previous_mark": cyc,
            "requests_stamped": int(len(rows)), "host_p50_us": ts[len(ts) // 2], "host_p99_us": ts[int(len(ts) * 0.99)],
            "median_from_request_seen": med,
+           "median_answer_to_next_seen_us": round(float(np.median(gaps)), 3)}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+def wide(args, st, ts, np, kernel):
+    """policy_wide_kernel stamps (r06, resident_wide.hip W_STAMP; 100 MHz wall clock) of
+    workgroups 0 and 17 (another XCD), per request: 0 request seen by the workgroup's
+    polling wave, 1 layer 0 done (first compute wave), 2 + l sliced layer l's input in
+    registers (l >= 1: after the granule sweep), 6 the last sliced layer's outputs in
+    LDS, 7 the head partials published, 8 every workgroup's partials gathered
+    (workgroup 0), 9 the answer stored. Times relative to workgroup 0 seeing the request."""
+    rows = st[(st[:, 0] > 0) & (st[:, 9] > 0)]
+    rel = (rows - rows[:, 0:1]) * 10.0 / 1e3
+    names = {0: "request seen", 1: "layer0 done", 3: "layer2 input swept", 4: "layer3 input swept",
+             6: "last sliced layer stored", 7: "partials published", 8: "partials gathered", 9: "answer stored"}
+    med = {}
+    for base, wgn in ((0, "wg0"), (16, "wg17")):
+        for s_, nm in names.items():
+            ok = rows[:, base + s_] > 0
+            if ok.sum() >= len(rows) // 2:
+                med[f"{wgn} {nm}"] = round(float(np.median(rel[ok, base + s_])), 3)
+    med = dict(sorted(med.items(), key=lambda kv: kv[1]))
+    gaps = (rows[1:, 0] - rows[:-1, 9]) * 10.0 / 1e3
+    out = {"model": args.model, "kernel": kernel, "requests_stamped": int(len(rows)),
+           "host_p50_us": ts[len(ts) // 2], "host_p99_us": ts[int(len(ts) * 0.99)],
+           "median_us_from_wg0_seen": med,
            "median_answer_to_next_seen_us": round(float(np.median(gaps)), 3)}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
