@@ -233,6 +233,8 @@ struct go2pi_engine {
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
   bool wide = false;          // act() form for wide policies (resident_wide.hip policy_wide_kernel, r06)
+  bool no_evict = false;      // GO2PI_RES_NO_EVICT=1 at create: this engine's batched launches evict no resident
+                              // kernel of another engine (A/B diagnostics; tests/test_gpu_resident.py)
   bool ctl_gran_ok = false;   // ... answered in granules (policy_act1_kernel, r05): no done word per tick
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // request granules: host view, device view
@@ -668,8 +670,7 @@ unsigned *yield_word(int device) {
 // at most GO2PI_YIELD_MIN_GRID workgroups fits beside the resident kernels and evicts
 // none (the kernels' own yield bump has the same bound, program.hpp).
 void evict_residents(const go2pi_engine *self, int64_t batch) {
-  static const bool off = std::getenv("GO2PI_RES_NO_EVICT") != nullptr;
-  if (off || (batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS <= GO2PI_YIELD_MIN_GRID) return;
+  if (self->no_evict || (batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS <= GO2PI_YIELD_MIN_GRID) return;
   std::lock_guard<std::mutex> lk(g_res_mu);
   for (go2pi_engine *o : g_res_engines)
     if (o != self && o->device == self->device && o->res_flag.load() == 1)
@@ -1071,12 +1072,6 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     // The general body (recurrent policies) takes both only together.
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
     if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
-    // the 8-wave lean kernel (two waves per SIMD) for 512-wide policies: GO2PI_W8=1 (A/B, r05)
-    {
-      const char *w8 = std::getenv("GO2PI_W8");
-      p.w4_nw = (p.w4_tpw == 8 && p.w4_plain && p.w4_actc == 1 && p.w4_nhc == 3 && p.head_fuse <= 1 && w8 &&
-                 w8[0] == '1') ? 8 : 4;
-    }
     // the lean GRU tick (policy_gru_kernel, r05): a GRU cell (lbr = 1) in front of
     // a dense chain the lean kernel would serve (gru_lean_on: GO2PI_GRU_LEAN / GO2PI_GRU_GENERAL)
     p.w4_gru_lean = (p.has_gru && p.gru.cell == 0 && p.gru.lbr == 1 && (p.gru.H == 128 || p.gru.H == 256) &&
@@ -1091,6 +1086,10 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, false) && !std::getenv("GO2PI_RES_MULTI");
   e.resident1_ctl = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, true) && !std::getenv("GO2PI_RES_MULTI");
   e.ctl_gran_ok = e.resident1_ctl && go2pi::resident1_ctl_granules(p);
+  e.no_evict = std::getenv("GO2PI_RES_NO_EVICT") != nullptr;
+  // the controller tick's general body instead of the lean tick kernel (A/B diagnostics,
+  // tests/test_gpu_controller.py::test_controller_tick_bodies)
+  p.ctl_general = std::getenv("GO2PI_CTL_GENERAL") != nullptr ? 1 : 0;
   // a wide dense policy (every hidden layer 256 or 512 wide: BASELINE configs[1]'s
   // 48 -> 512^3 -> 12) is served by policy_wide_kernel when every workgroup can poll the
   // request ring in device memory (large BAR); else by the multi-workgroup kernel, whose
@@ -1700,12 +1699,8 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     if (t && e->prog.w4_gru_lean)  // the lean GRU tick: <tiles per wave, head tiles, hidden tiles per wave>
       std::snprintf(buf, cap, "policy_gru_kernel<%d, %d, %d>", t, h, e->prog.gru.H / 64);
     else if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
-                                // act, hidden layers>
-      // (<..., waves per workgroup>: 4, or 8 with half the tiles per wave)
-      if (e->prog.w4_nw == 8)
-        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 8>", t / 2, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
-      else
-        std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 4>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
+                                     // act, hidden layers, waves per workgroup (4)>
+      std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 4>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);
     else
       std::snprintf(buf, cap, "policy_fused_kernel<%d, %d, %d, %d, %d, %d, %d>", e->waves, t, h, c0m,
                     (e->prog.has_gru && e->prog.gru.cell == 1) ? 1 : 0, t ? e->prog.w4_actc : -1,

@@ -109,8 +109,8 @@ struct DevProgram {
   int w4_bias;     // pipeline: LDS floats holding every hidden layer's bias (sum of their N_pad), else 0
   const float *w4_bpack;  // pipeline: those biases packed back to back in device memory (one LDS-DMA stream)
   int w4_plain;           // pipeline, 1: no prologue / epilogue arithmetic, no recurrent cell (the lean kernel)
-  int w4_nw;              // lean kernel's waves per workgroup: 4 (one per SIMD) or 8 (two per SIMD, TPW / 2 tiles each; r05)
   int w4_gru_lean;        // 1: a GRU policy served by the lean GRU tick (policy_gru_kernel, r05)
+  int ctl_general;        // 1: the controller tick runs the general body, not the lean tick kernel (A/B)
   int w4_c0m;             // pipeline: layer 0's k-chunks mod 4 (0 or 3; K padded to 16, not 64, when 3)
   int w4_actc;            // lean kernel: the hidden activation as a compile-time constant (1 = Elu), or -1
   int w4_nhc;             // lean kernel: the hidden-layer count as a compile-time constant (3), or 0 (runtime)

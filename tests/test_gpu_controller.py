@@ -86,6 +86,20 @@ def test_controller_history_lengths(synth_path, name, hist, B, res):
         _run_ticks(e, _mlp_policy(p), B, 3, seed=B + hist, hist=hist)
 
 
+@pytest.mark.parametrize("env", [{}, {"GO2PI_CTL_GENERAL": "1"}])
+@pytest.mark.parametrize("name,hist", [("shipped", 2), ("ctl_h3_deep", 3)])
+def test_controller_tick_bodies(synth_path, monkeypatch, env, name, hist):
+    """The batched controller tick in both bodies: the lean tick kernel (policy_mlp_ctl_kernel,
+    the default for Elu policies with three hidden layers) and the general body
+    (GO2PI_CTL_GENERAL=1 at create, A/B), bit-exact observations and oracle actions."""
+    from go2_onnx_controller_amd import Engine
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)  # read at engine creation
+    p = SHIPPED if name == "shipped" else synth_path(name)
+    with Engine(p, max_batch=300) as e:
+        _run_ticks(e, _mlp_policy(p), 300, 3, seed=hist + len(env), hist=hist)
+
+
 @pytest.mark.parametrize("waves", [4, 16])
 def test_controller_waves(waves):
     from go2_onnx_controller_amd import Engine

@@ -114,3 +114,39 @@ def test_pipeline_body_and_layer0_variants(synth_path, monkeypatch, name, env, k
             assert args[4] == nhc, k
         for B in (5, 16, 4096):
             assert abs_err(e.run(x[:B]), onnx_ref.act(g, x[:B])) <= TOL, (B, env)
+
+
+@pytest.mark.parametrize("env", [{"GO2PI_NO_W4": "1"}, {"GO2PI_NO_HEAD_FUSE": "1"}])
+@pytest.mark.parametrize("name", ["go2_mlp_512", "pipe_256_h2"])
+def test_generic_body_switches(synth_path, monkeypatch, env, name):
+    """The generic 8-wave body the engine falls back to when the pipeline is switched off
+    (GO2PI_NO_W4=1), and without the head fused into the last hidden layer
+    (GO2PI_NO_HEAD_FUSE=1, which also keeps the pipeline off): A/B switches read at
+    create, each against the fp64 oracle."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = synth_path(name)
+    g = onnx_ref.load(p)
+    x = np.random.default_rng(13).standard_normal((4096, g.inputs[0][1][1])).astype(np.float32)
+    with Engine(p, max_batch=4096, small_batch=-1) as e:
+        assert e.batched_kernel.startswith("policy_fused_kernel<8, 0, 0,"), e.batched_kernel
+        for B in (5, 16, 300, 4096):
+            assert abs_err(e.run(x[:B]), onnx_ref.act(g, x[:B])) <= TOL, (B, env)
+
+
+def test_small_chain_switch(synth_path, monkeypatch):
+    """GO2PI_SMALL_CHAIN=1 at create: batches <= 8 by the GEMV chain (one launch per layer,
+    replayed as a hipGraph) instead of the single-launch latency kernel, against the fp64
+    oracle; larger batches are unaffected."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import onnx_ref
+    monkeypatch.setenv("GO2PI_SMALL_CHAIN", "1")
+    for name in ("go2_mlp_512", "pipe_one_hidden"):
+        p = synth_path(name)
+        g = onnx_ref.load(p)
+        x = np.random.default_rng(17).standard_normal((64, g.inputs[0][1][1])).astype(np.float32)
+        with Engine(p, max_batch=64, small_batch=8) as e:
+            for B in (1, 2, 8, 9, 64, 1):
+                assert abs_err(e.run(x[:B]), onnx_ref.act(g, x[:B])) <= TOL, (name, B)
