@@ -561,6 +561,11 @@ def main():
             if cpp:
                 cpp["what"] = ("ONNXActor::act() at batch 1 timed in C++ (steady_clock around one call, "
                                "main.cpp:38-42), resident kernel, 1,000 warm + 10,000 timed calls")
+                from go2_onnx_controller_amd import Engine as _Engine
+                for name, path in (("go2_mlp_512", model_path), ("shipped", shipped)):
+                    if name in cpp:  # the resident form each model gets (no launch: the name only)
+                        with _Engine(path, device=local, max_batch=8, resident_ms=100) as _e:
+                            cpp[name]["resident_kernel"] = _e.resident_kernel
                 out["latency_b1_act_cpp"] = cpp
             # the recurrent policy (configs[4]'s GRU-256) at batch 1: the resident kernel's GRU
             # form (hidden rows carried inside the live kernel), then one fused launch per call

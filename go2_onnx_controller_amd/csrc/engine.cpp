@@ -1072,9 +1072,11 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
     // The general body (recurrent policies) takes both only together.
     p.w4_nhc = (p.w4_actc == 1 && p.nl - 1 == 3 && !std::getenv("GO2PI_LEAN_RT_NH")) ? 3 : 0;  // env: A/B only
     if (!p.w4_plain && p.w4_nhc == 0) p.w4_actc = -1;
-    // the lean GRU tick (policy_gru_kernel, r05): a GRU cell (lbr = 1) in front of
-    // a dense chain the lean kernel would serve (gru_lean_on: GO2PI_GRU_LEAN / GO2PI_GRU_GENERAL)
-    p.w4_gru_lean = (p.has_gru && p.gru.cell == 0 && p.gru.lbr == 1 && (p.gru.H == 128 || p.gru.H == 256) &&
+    // the lean recurrent tick (policy_gru_kernel, r05; policy_lstm_kernel, r06): a GRU cell
+    // (lbr = 1) or an LSTM cell in front of a dense chain the lean kernel would serve
+    // (gru_lean_on: GO2PI_GRU_GENERAL=1 keeps the general body for both cells, A/B)
+    p.w4_gru_lean = (p.has_gru && ((p.gru.cell == 0 && p.gru.lbr == 1) || p.gru.cell == 1) &&
+                     (p.gru.H == 128 || p.gru.H == 256) &&
                      p.gru.H <= 64 * p.w4_tpw && !p.pre_sub && !p.pre_div && !p.pre_mul && !p.pre_clip &&
                      p.post_plain && p.lds_stride == 64 * p.w4_tpw + 4 && p.w4_actc == 1 && p.w4_nhc == 3 &&
                      p.c0 == p.gru.H / 16 && p.gru.I_pad == (p.in_dim + 63) / 64 * 64 && p.in_dim < 4096 &&
@@ -1696,8 +1698,9 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     if (!buf || cap == 0) throw ApiError("null buffer", GO2PI_E_INVALID);
     const int t = e->waves == 4 ? e->prog.w4_tpw : 0, h = t ? e->prog.head_fuse : 0;
     const int c0m = t ? e->prog.w4_c0m : 0;
-    if (t && e->prog.w4_gru_lean)  // the lean GRU tick: <tiles per wave, head tiles, hidden tiles per wave>
-      std::snprintf(buf, cap, "policy_gru_kernel<%d, %d, %d>", t, h, e->prog.gru.H / 64);
+    if (t && e->prog.w4_gru_lean)  // the lean GRU / LSTM tick: <tiles per wave, head tiles, hidden tiles per wave>
+      std::snprintf(buf, cap, "%s<%d, %d, %d>", e->prog.gru.cell == 1 ? "policy_lstm_kernel" : "policy_gru_kernel", t,
+                    h, e->prog.gru.H / 64);
     else if (t && e->prog.w4_plain)  // the lean pipeline kernel: <tiles per wave, head tiles, layer-0 chunks mod 4,
                                      // act, hidden layers, waves per workgroup (4)>
       std::snprintf(buf, cap, "policy_mlp_kernel<%d, %d, %d, %d, %d, 4>", t, h, c0m, e->prog.w4_actc, e->prog.w4_nhc);

@@ -1649,13 +1649,19 @@ __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &c
 // arguments, so the observation rows, the hidden rows (16-byte direct-to-LDS loads: one
 // per 256 units of a row) and the cell's first fragments go out at once. Gate biases,
 // the program and yield come from the argument segment.
-template <int TPW, int HT, int GT>
+// LSTM (r06, the lean LSTM tick): the same body around the
+// four-gate cell (w4_lstm, ONNX gates i, o, f, c; gbzr = Wb + Rb per gate). A state row
+// is h | c (2H floats): the h half goes to LDS as the GRU's hidden row does, and each
+// lane's c units (the units of its own h' outputs) to registers, where the cell keeps
+// them across every tick of the launch; both halves go back to the state rows once.
+template <int TPW, int HT, int GT, bool LSTM = false>
 __device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *obs, float *act, float *hidden,
                                             const float *gw, const float *l0w, const float *bpack, unsigned shape,
                                             const float *gbzr, const float *gbh, int steps, unsigned *yield) {
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   constexpr int H = 64 * GT, S = 64 * TPW + 4, NBIAS = 3 * 64 * TPW;
+  constexpr int SW = LSTM ? 2 * H : H;  // state floats per robot row
   static_assert(H <= 64 * TPW, "the hidden rows fit the LDS row");
   const int B = (int)(shape & 0xFFFFFu), in_dim = (int)(shape >> 20);
   const int ipad = (in_dim + 63) & ~63, nch = ipad >> 6;  // (pack_gru: x padded to whole 64-column groups)
@@ -1683,7 +1689,7 @@ __device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *ob
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = wave + 4 * i;
-    const float *hp = hidden + (size_t)min(row0 + r, B - 1) * H;
+    const float *hp = hidden + (size_t)min(row0 + r, B - 1) * SW;
     if constexpr (H % 256 == 0) {
 #pragma unroll
       for (int c = 0; c < H / 256; ++c)
@@ -1703,19 +1709,33 @@ __device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *ob
     __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   GO2PI_STAMP(P, tid == 0, 0);
   GO2PI_STAMP_RT(P, tid == 0, 1);
-  const DevGru G{gw, gbzr, gbh, in_dim, ipad, H, 1, 0, H};
+  const DevGru G{gw, gbzr, gbh, in_dim, ipad, H, LSTM ? 0 : 1, LSTM ? 1 : 0, SW};
   const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, H / 16, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
+  // LSTM: this lane's cell-state units, in registers for every tick (rows past B: zeros)
+  float4 creg[LSTM ? GT : 1];
+  if constexpr (LSTM) {
+    const int row = row0 + (lane & 15);
+    const float *cg = hidden + (size_t)min(row, B - 1) * SW + H + wave * GT * 16 + ((lane >> 4) << 2);
+#pragma unroll
+    for (int i = 0; i < GT; ++i)
+      creg[i] = row < B ? *reinterpret_cast<const float4 *>(cg + i * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   int ep = 0;
   for (int step = 0; step < steps; ++step) {
     if (step > 0) stage_obs(step);
     float4 ring0[4][TPW];  // the dense chain's layer-0 ring, filled behind the cell (w4_prefill)
     float4 hn[GT];
     auto mid = [&] { w4_prefill<TPW, 0>(l0w, ring0, wave, lane); };
-    w4_gru<GT>(G, bufA, bufH, bufB, S, wave, lane, hn, nullptr, mid);
+    if constexpr (LSTM) w4_lstm<GT>(G, bufA, bufH, bufB, S, wave, lane, hn, creg, mid);
+    else w4_gru<GT>(G, bufA, bufH, bufB, S, wave, lane, hn, nullptr, mid);
     if (step == steps - 1 && row0 + (lane & 15) < B) {  // the engine's state: once, from registers
-      float *hg = hidden + (size_t)(row0 + (lane & 15)) * H + wave * GT * 16 + ((lane >> 4) << 2);
+      float *hg = hidden + (size_t)(row0 + (lane & 15)) * SW + wave * GT * 16 + ((lane >> 4) << 2);
 #pragma unroll
       for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + i * 16) = hn[i];
+      if constexpr (LSTM) {
+#pragma unroll
+        for (int i = 0; i < GT; ++i) *reinterpret_cast<float4 *>(hg + H + i * 16) = creg[i];
+      }
     }
     lds_barrier();  // every wave has read bufH (an LDS hand-off: no wait for the ring's loads)
     float *hl = bufH + (lane & 15) * S + wave * GT * 16 + ((lane >> 4) << 2);
@@ -2105,6 +2125,18 @@ __global__ __launch_bounds__(256) void policy_gru_kernel(const float *__restrict
                                                          const DevProgram *__restrict__ Pd, int steps,
                                                          unsigned *yield) {
   w4_gru_body<TPW, HT, GT>(*Pd, obs, act, hidden, gw, l0w, bpack, shape, gbzr, gbh, steps, yield);
+}
+
+// The lean LSTM tick (w4_gru_body's LSTM form, r06): the same arguments (gbh unused).
+template <int TPW, int HT, int GT>
+__global__ __launch_bounds__(256) void policy_lstm_kernel(const float *__restrict__ obs, float *__restrict__ act,
+                                                          float *__restrict__ hidden, const float *__restrict__ gw,
+                                                          const float *__restrict__ l0w,
+                                                          const float *__restrict__ bpack, unsigned shape,
+                                                          const float *gbzr, const float *gbh,
+                                                          const DevProgram *__restrict__ Pd, int steps,
+                                                          unsigned *yield) {
+  w4_gru_body<TPW, HT, GT, true>(*Pd, obs, act, hidden, gw, l0w, bpack, shape, gbzr, gbh, steps, yield);
 }
 
 template <int NW, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0>

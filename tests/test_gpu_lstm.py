@@ -35,13 +35,19 @@ def _rollout(path, xs, h0=None, c0=None):
     return np.stack(ys), h[0], c[0]
 
 
-@pytest.mark.parametrize("name,waves,kernel", [("lstm_small", 0, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>"),
-                                               ("lstm_128", 0, "policy_fused_kernel<4, 4, 1, 0, 1, -1, 0>"),
-                                               ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1, 1, 3>"),
-                                               ("go2_lstm_256", 8, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>")])
+# go2_lstm_256 (LSTM-256 + 512^3 Elu head) takes the lean LSTM tick (policy_lstm_kernel,
+# r06); GO2PI_GRU_GENERAL=1 keeps the general body's pipelined LSTM stage
+@pytest.mark.parametrize("name,waves,kernel,general", [
+    ("lstm_small", 0, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>", False),
+    ("lstm_128", 0, "policy_fused_kernel<4, 4, 1, 0, 1, -1, 0>", False),
+    ("go2_lstm_256", 0, "policy_lstm_kernel<8, 1, 4>", False),
+    ("go2_lstm_256", 0, "policy_fused_kernel<4, 8, 1, 0, 1, 1, 3>", True),
+    ("go2_lstm_256", 8, "policy_fused_kernel<8, 0, 0, 0, 1, -1, 0>", False)])
 @pytest.mark.parametrize("B", [1, 37, 4096])
-def test_lstm_ticks(synth_path, name, waves, kernel, B):
+def test_lstm_ticks(synth_path, monkeypatch, name, waves, kernel, general, B):
     from go2_onnx_controller_amd import Engine
+    if general:
+        monkeypatch.setenv("GO2PI_GRU_GENERAL", "1")  # read at engine creation
     p = synth_path(name)
     rng = np.random.default_rng(B + waves)
     with Engine(p, max_batch=max(B, 64), waves=waves) as e:
