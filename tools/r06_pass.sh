@@ -23,4 +23,10 @@ if [ -f $R/go2_onnx_controller_amd/lib/diag/libgo2pi_clock.so ]; then
   python3 -c "import json; d=json.load(open('$O/clock_mlp512.json')); print({k: d[k] for k in ('wg_us_median','launch_span_us','event_us_per_launch','wg_start_spread_us','wg_end_spread_us','phase_cycles_median')})"
 fi
 [ -n "$NO_BENCH" ] || { timeout -k 10 600 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }; cat $O/bench.json; }
+if [ -z "$NO_BENCH" ]; then  # the recurrent one-tick lines (lean GRU / LSTM ticks)
+  for w in go2_gru_256_b4096 go2_lstm_256_b4096; do
+    timeout -k 10 300 python3 $R/bench.py --workload $w --no-cpu --no-latency --no-ctl --no-gru > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail -20 $O/bench_$w.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_$w.json')); print('$w', d['ms_per_step'], d['roofline']['frac'], d['config'])"
+  done
+fi
 echo "r06_pass ok"
