@@ -30,8 +30,9 @@
 //    per CU, each output's granule stored by its own row's lane, lost granules of whole
 //    waves under load: the line written piecewise by 8 waves);
 //  * the head (<= 16 outputs) is split over the workgroups by k: workgroup p multiplies
-//    its 16 last-layer outputs by the head's columns [16 p, 16 p + 16) and publishes
-//    16 partial sums; workgroup 0 sums the P partials of each output in a fixed order
+//    its 16 last-layer outputs by the head's columns [16 p, 16 p + 16) (each row of the
+//    last sliced layer: its output times the column, lane s for head output s, into
+//    LDS) and its communication wave sums and publishes the 16 partials; workgroup 0 sums the P partials of each output in a fixed order
 //    (the second and last crossing; its communication wave sweeps them), adds the bias,
 //    applies the head's activation and the action epilogue, and answers as {epoch,
 //    value} granules in host memory.
@@ -39,8 +40,9 @@
 // Summation order (deterministic, within the 1e-5 contract of the fp64 oracle; not the
 // MFMA path's order): layer 0 two packed fma chains per output; a sliced layer two
 // packed chains per lane, the fixed DPP tree, then the row pair; the head per
-// workgroup the DPP tree over its 16 columns, then the partials in workgroup order
-// p = q + 4u (u ascending within each of four lane groups q, then q by xor 16, xor 32).
+// workgroup its 16 column products in column order, then the partials in workgroup
+// order p = q + 4u (u ascending within each of four lane groups q, then q by xor 16,
+// xor 32).
 //
 // Leaving: a LEAVE request header, idle_ticks without a request, a moved yield
 // counter, or the launch's abort word (set by a communication wave whose granule sweep
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(64 * (1 + CW)) void policy_wide_kernel(const DevPro
   float *h0 = x0 + MB * S0;                     // [8][H] layer 0's outputs
   float *hh = h0 + MB * H;                      // [8][H] a sliced layer's outputs of every workgroup (swept)
   float *ho = hh + MB * H;                      // [8][16] this workgroup's outputs of a sliced layer
-  float *pp = ho + MB * 16;                     // [8][16] its head partials
+  float *pp = ho + MB * 16;                     // [8][16 columns][16 head outputs] its head products
   int *st = reinterpret_cast<int *>(pp + MB * 16);  // [0] leave [1] epoch [2] batch [3] fail
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -264,9 +266,9 @@ __global__ __launch_bounds__(64 * (1 + CW)) void policy_wide_kernel(const DevPro
       for (int f = 0; f < 4; ++f) wm[l][f] = w_ld(P.L[1 + l], 16 * wg + o, kb + 4 * f);
       bm[l] = P.L[1 + l].bias[16 * wg + o];
     }
-    if (g < 16) {  // the head's column 16 wg + s of output g
-      const float4 w = w_ld(P.L[NL - 1], g, (16 * wg + s) & ~3);
-      const int r = s & 3;
+    {  // the head's weight of output s at column 16 wg + o (the row's last-layer output)
+      const float4 w = w_ld(P.L[NL - 1], s, (16 * wg + o) & ~3);
+      const int r = o & 3;
       wh = r == 0 ? w.x : (r == 1 ? w.y : (r == 2 ? w.z : w.w));
     }
   } else {
@@ -383,7 +385,13 @@ __global__ __launch_bounds__(64 * (1 + CW)) void policy_wide_kernel(const DevPro
           float p[1] = {acc.x + acc.y};
           float v = a1_reduce<1>(p);
           if constexpr (RPO == 2) v = w_pair_add(v);
-          if (s == 0 && kh == RPO - 1) ho[b * 16 + o] = act_fn(A, lal[1 + l], lbe[1 + l], v + bm[l]);
+          if (l + 1 < NS) {
+            if (s == 0 && kh == RPO - 1) ho[b * 16 + o] = act_fn(A, lal[1 + l], lbe[1 + l], v + bm[l]);
+          } else if (kh == RPO - 1) {
+            // the last sliced layer: its output o times the head's column, for every head
+            // output s (lane s of the row; the row's lanes all hold the output)
+            pp[(b * 16 + o) * 16 + s] = wh * act_fn(A, lal[1 + l], lbe[1 + l], v + bm[l]);
+          }
         }
       }
       if (l + 1 < NS) {
@@ -407,18 +415,23 @@ __global__ __launch_bounds__(64 * (1 + CW)) void policy_wide_kernel(const DevPro
       }
     }
     W_STAMP(64, 6);
-    lds_barrier();  // this workgroup's outputs of the last sliced layer in ho
-    // ---- the head's partial sums over this workgroup's 16 columns (row g: output g)
-    if (wave != 0 && g < 16 && st[3] == 0) {
-      for (int b = 0; b < B; ++b) {
-        float p[1] = {wh * ho[b * 16 + s]};
-        const float v = a1_reduce<1>(p);
-        if (s == 0) pp[b * 16 + g] = v;
-      }
-    }
-    lds_barrier();  // the partials in pp
+    lds_barrier();  // the head products of this workgroup's 16 columns in pp
     if (wave == 0 && st[3] == 0) {
-      publish(pp, part, (size_t)NP * 16, B, e + (unsigned)NL - 1u);
+      // ---- the head's partial sums over this workgroup's 16 columns: lane 16 b' + j sums
+      // output j's 16 products of row b (columns o = 0 .. 15 in order) and stores it; the
+      // lanes of a row store its 16 partials, one 128-byte line, in one instruction
+#pragma unroll
+      for (int i0 = 0; i0 < 16 * MB; i0 += 64) {
+        const int i = i0 + lane, b = i >> 4, j = i & 15;
+        if (b < B) {
+          const float *pr = pp + b * 256 + j;
+          float a = 0.f;
+#pragma unroll
+          for (int oo = 0; oo < 16; ++oo) a += pr[oo * 16];
+          __hip_atomic_store(part + ((size_t)b * NP + wg) * 16 + j, ((u64)(e + (unsigned)NL - 1u) << 32) | __float_as_uint(a),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       W_STAMP(0, 7);
       // ---- workgroup 0: the partials of every workgroup summed, the answer
       if (wg == 0) {
@@ -494,7 +507,7 @@ WideShape wide_shape(const DevProgram &p) {
 }
 
 size_t wide_lds_bytes(const WideShape &w) {
-  return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * (4 * w.f0 + 2 * 64 * w.cw + 32) + 4);
+  return sizeof(float) * ((size_t)GO2PI_SMALL_MAXB * (4 * w.f0 + 2 * 64 * w.cw + 16 + 256) + 4);
 }
 
 int launch_resident_wide(const DevProgram &p, const DevProgram *p_dev, const unsigned long long *req,

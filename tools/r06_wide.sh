@@ -9,10 +9,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/wide
 mkdir -p $O $R/build
 L=$R/go2_onnx_controller_amd/lib
-timeout -k 10 600 python3 -u -m pytest $R/tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread \
+[ -n "$SEL_SKIP" ] || timeout -k 10 600 python3 -u -m pytest $R/tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread \
   -k "${SEL:-wide or ring or mlp512 or two_engines or destroy or interleaved or prologue}" > $O/tests.log 2>&1 \
   || { echo "tests failed"; grep -E "FAILED|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
+[ -n "$SEL_SKIP" ] || tail -3 $O/tests.log
 g++ -std=c++20 -O2 -I$R/include $R/tests/cpp/controller_shape.cpp -L$L -lonnx_actor -Wl,-rpath,$L -o $R/build/controller_shape || exit 1
 M512=$(python3 -c "import sys; sys.path.insert(0, '$R'); from go2_onnx_controller_amd import synth; print(synth.ensure_model('go2_mlp_512'))")
 for round in 1 2 3; do
