@@ -233,6 +233,7 @@ struct go2pi_engine {
   bool resident1 = false;     // act() form in one workgroup (resident.hip policy_resident1_kernel)
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
   bool wide = false;          // act() form for wide policies (resident_wide.hip policy_wide_kernel, r06)
+  int64_t res_launches = 0;   // resident kernel launches (go2pi_resident_launches)
   bool no_evict = false;      // GO2PI_RES_NO_EVICT=1 at create: this engine's batched launches evict no resident
                               // kernel of another engine (A/B diagnostics; tests/test_gpu_resident.py)
   bool ctl_gran_ok = false;   // ... answered in granules (policy_act1_kernel, r05): no done word per tick
@@ -369,6 +370,7 @@ struct go2pi_engine {
       hip_check(go2pi::launch_resident(prog, d_prog, m_req, m_actg, d_gran, gstride, d_mirror, m_err, m_done,
                                        res_idle_ticks, ctl, d_hgran, d_hidden, prog.yield, stream),
                 "resident launch");
+    ++res_launches;
     resident_live = true;
     res_flag.store(1);
     resident_ctl = ctl != nullptr;
@@ -1729,6 +1731,15 @@ int go2pi_resident_kernel(const go2pi_engine *e, char *buf, size_t cap) {
     } else {
       std::snprintf(buf, cap, "policy_resident_kernel%s", ring);
     }
+    return GO2PI_OK;
+  });
+}
+
+int go2pi_resident_launches(const go2pi_engine *e, int64_t *n) {
+  return guarded([&] {
+    check_engine(e);
+    if (!n) throw ApiError("null argument", GO2PI_E_INVALID);
+    *n = e->res_launches;
     return GO2PI_OK;
   });
 }

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(64 * (1 + CW)) void policy_wide_kernel(const DevPro
   float *hh = h0 + MB * H;                      // [8][H] a sliced layer's outputs of every workgroup (swept)
   float *ho = hh + MB * H;                      // [8][16] this workgroup's outputs of a sliced layer
   float *pp = ho + MB * 16;                     // [8][16 columns][16 head outputs] its head products
-  int *st = reinterpret_cast<int *>(pp + MB * 16);  // [0] leave [1] epoch [2] batch [3] fail
+  int *st = reinterpret_cast<int *>(pp + MB * 256);  // [0] leave [1] epoch [2] batch [3] fail
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wg = blockIdx.x;

@@ -22,7 +22,7 @@ EXPORTS = [
     "go2pi_io_name", "go2pi_io_shape", "go2pi_io_dims", "go2pi_run", "go2pi_run_device",
     "go2pi_run_sequence_device", "go2pi_reset_hidden", "go2pi_get_hidden", "go2pi_set_hidden",
     "go2pi_hidden_dim", "go2pi_sync", "go2pi_get_cost", "go2pi_batched_kernel", "go2pi_inspect_model",
-    "go2pi_diag_stamps", "go2pi_resident_kernel",
+    "go2pi_diag_stamps", "go2pi_resident_kernel", "go2pi_resident_launches",
     "go2pi_last_error", "go2pi_version", "go2pi_ctl_default_params", "go2pi_ctl_set_params",
     "go2pi_ctl_history", "go2pi_controller_step", "go2pi_controller_step_device",
 ]
@@ -123,6 +123,7 @@ def lib():
             "go2pi_get_cost": (ctypes.c_int, [P, P]),
             "go2pi_batched_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_resident_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_size_t]),
+            "go2pi_resident_launches": (ctypes.c_int, [P, P]),
             "go2pi_diag_stamps": (ctypes.c_int, [P, P, I64]),
             "go2pi_inspect_model": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
             "go2pi_last_error": (ctypes.c_char_p, []),
@@ -134,7 +135,7 @@ def lib():
             "go2pi_controller_step_device": (ctypes.c_int, [P, P, P, P, P, P, P, P, P, I64, P]),
         }
         for name, (res, args) in sig.items():
-            if name in ("go2pi_batched_kernel", "go2pi_resident_kernel") and not hasattr(L, name) and \
+            if name in ("go2pi_batched_kernel", "go2pi_resident_kernel", "go2pi_resident_launches") and not hasattr(L, name) and \
                     os.environ.get("GO2PI_LIB"):
                 continue  # an older diagnostics build (A/B tooling): the name query is optional there
             fn = getattr(L, name)
@@ -214,6 +215,14 @@ class Engine:
             kb = ctypes.create_string_buffer(128)
             _check(L.go2pi_resident_kernel(h, kb, 128))
             self.resident_kernel = kb.value.decode()  # e.g. "policy_wide_kernel<4, 8, 12, 0> ring=vram"
+
+    @property
+    def resident_launches(self):
+        """Resident kernel launches so far (go2pi_resident_launches): one per idle-out,
+        stop or abort; a kernel that gives up on every request shows as one per call."""
+        n = ctypes.c_int64(0)
+        _check(lib().go2pi_resident_launches(self._h, ctypes.byref(n)))
+        return n.value
 
     def _io(self, is_out, k):
         L = lib()

@@ -141,6 +141,11 @@ int go2pi_batched_kernel(const go2pi_engine *e, char *buf, size_t cap);
    compute. */
 int go2pi_resident_kernel(const go2pi_engine *e, char *buf, size_t cap);
 
+/* Resident kernel launches this engine has made so far (one serves every request
+   until it idles out or another call stops it; a kernel that aborts on a request
+   shows up as a launch per call). For tests and profiling tools; no compute. */
+int go2pi_resident_launches(const go2pi_engine *e, int64_t *n);
+
 /* Parse and lower an ONNX policy WITHOUT touching a device (no compute): writes a
    JSON description (I/O names and shapes, the lowered layer program with
    per-layer weight/bias checksums) into buf. Returns the JSON length (>= 0) or an

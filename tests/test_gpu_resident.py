@@ -79,6 +79,33 @@ def test_resident_vs_launch_per_call(synth_path, name, form, monkeypatch):
             assert abs_err(y, ref.f64(x)) <= TOL
 
 
+@pytest.mark.parametrize("name,form", [("shipped", "one"), ("shipped", "multi"), ("mlp512", "multi"),
+                                       ("mlp512", "wide"), ("wide_256_3", "wide"), ("wide_256_4", "wide"),
+                                       ("wide_512_3", "wide")])
+def test_resident_kernel_stays_live(synth_path, name, form, monkeypatch):
+    """One resident launch serves a run of requests at batch 1..8 (go2pi_resident_launches):
+    a kernel that gives up on every request (a failed sweep, a clobbered LDS word) still
+    answers correctly through a relaunch per call, so parity alone does not show it."""
+    from go2_onnx_controller_amd import Engine
+    from oracle import mlp_ref
+    if form == "multi":
+        monkeypatch.setenv("GO2PI_RES_MULTI", "1")  # read at engine creation
+    path = _models(synth_path)[name]
+    ref = mlp_ref.MlpRef.from_onnx(path)
+    rng = np.random.default_rng(11)
+    with Engine(path, max_batch=8, resident_ms=5000) as e:
+        if e.resident_kernel == "none":
+            pytest.skip("no resident form for this model")
+        assert e.resident_launches == 0
+        for i, B in enumerate([1, 8, 1, 1, 3, 1, 8, 1] * 25):
+            x = (realistic_obs(B, seed=i) if name == "shipped"
+                 else rng.standard_normal((B, e.in_dim)).astype(np.float32))
+            y = e.run(x)
+            if i % 20 == 0:
+                assert abs_err(y, ref.f64(x)) <= TOL, f"call {i} B={B}"
+        assert e.resident_launches == 1, f"{e.resident_kernel}: {e.resident_launches} launches for 200 requests"
+
+
 def test_resident_known_answers():
     """The reference drivers' inputs (src/cpp/main.cpp:32 zeros, src/python/main.py:20 twos)."""
     import os
