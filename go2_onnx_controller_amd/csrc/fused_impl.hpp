@@ -22,7 +22,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // the 4-wave pipeline's ring depth by tiles per wave: a chunk is 4 * TPW MFMAs
 // (32 cycles each), and a fragment must be issued >= ~1K cycles (an L2 round trip
 // under load) before its MFMA
-#define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? 1 : ((TPW) >= 4 ? 2 : 3))
+#ifndef GO2PI_W4_RD8
+#define GO2PI_W4_RD8 1
+#endif
+#define GO2PI_W4_RD(TPW) ((TPW) >= 8 ? GO2PI_W4_RD8 : ((TPW) >= 4 ? 2 : 3))
 #define GO2PI_FLAG_FLOATS 64  // LDS words for the per-wave layer hand-off flags (<= 64 waves)
 
 // Diagnostic ablation builds only (tools/bound_probe.sh; outputs are wrong by design):
@@ -750,7 +753,9 @@ __device__ __forceinline__ void lstm_cell(const DevGru &G, const float *X, const
 // Load spacing: one fragment load after every LSP-th MFMA, so the chunk's TPW
 // loads are issued over its first LSP * TPW MFMAs (the earlier they go out, the
 // longer the last tile's fragment has before its MFMA in the next chunk).
+#ifndef GO2PI_W4_LSP
 #define GO2PI_W4_LSP 2
+#endif
 template <int TPW, int S, int RD, bool LOAD, bool PIN>
 __device__ __forceinline__ void w4_chunk(f32x4 (&acc)[TPW], float4 (&f)[4][TPW], const float4 &b, const WStream &ws,
                                          const int (&vo)[TPW], int soff) {
@@ -784,10 +789,13 @@ __device__ __forceinline__ float4 w4_epi(const ActP &ap, const f32x4 &acc, const
 // The lean kernel's Elu epilogue (ACTC == 1: Elu with alpha = 1, the exported
 // policies'): the bias is already in the accumulator (BIN: the first MFMA of each
 // tile took it as its C operand), and the x * log2(e) and e - 1 steps run as
-// packed pairs. Per element the same operations as act_t<1> with alpha = 1
-// (x > 0 ? x : exp2(x * log2 e) - 1), so the same bits for the same x.
+// packed pairs. Per element the value of act_t<1> with alpha = 1 (x > 0 ? x :
+// exp2(x * log2 e) - 1), the same bits for the same x (x = -0 aside, below).
 // (A select-free form, max(x, clamp(e, 0, 1) - 1), measured 0.4 % faster but maps
-// a NaN to -1 where ONNX Elu propagates it: rejected)
+// a NaN to -1 where ONNX Elu propagates it: rejected, DESIGN §4.1. The integer min
+// below propagates it.)
+// r06 A/B (profiles/r06_ab_epi.txt): VGPR accumulators + the integer min, mlp512
+// 35.43 -> 35.02-35.12 us, GRU-256 tick 57.0 -> 56.4-56.5 us.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool BIN>
 __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv) {
@@ -796,21 +804,28 @@ __device__ __forceinline__ float4 w4_epi_elu1(const f32x4 &acc, const float4 &bv
     x01 += f32x2{bv.x, bv.y};
     x23 += f32x2{bv.z, bv.w};
   }
-  // one copy out of the accumulator registers per element (the scheduler otherwise
-  // re-reads an AGPR for the select; VALU here is not hidden behind the MFMAs:
-  // tools/mfma_valu.hip, every instruction counts)
-  asm volatile("" : "+v"(x01), "+v"(x23));
+  // (r06: the accumulators are VGPRs, the pipeline units are built with
+  // -amdgpu-mfma-vgpr-form: no accvgpr read in front of each element, and no copy)
   const f32x2 L = {1.4426950408889634f, 1.4426950408889634f};
   const f32x2 t01 = x01 * L, t23 = x23 * L;
   f32x2 e01 = {__builtin_amdgcn_exp2f(t01.x), __builtin_amdgcn_exp2f(t01.y)};
   f32x2 e23 = {__builtin_amdgcn_exp2f(t23.x), __builtin_amdgcn_exp2f(t23.y)};
   e01 -= 1.f;
   e23 -= 1.f;
+  // The select x > 0 ? x : e - 1 as one signed-integer min of the bit patterns (r06,
+  // one v_min_i32 instead of a compare and a select): x > 0 (and +inf, and a NaN of
+  // either sign) has e - 1 >= x with the same sign, so the smaller pattern is x; x <= 0
+  // has x <= e - 1 <= 0, and negative patterns order by magnitude, so the min is e - 1
+  // (x = -inf: -1). Bitwise the compare + select's result except at x = -0, which
+  // gives -0 where the select gives +0.
+  auto imin = [](float a, float b) {
+    return __int_as_float(__builtin_elementwise_min(__float_as_int(a), __float_as_int(b)));
+  };
   float4 v;
-  v.x = x01.x > 0.f ? x01.x : e01.x;
-  v.y = x01.y > 0.f ? x01.y : e01.y;
-  v.z = x23.x > 0.f ? x23.x : e23.x;
-  v.w = x23.y > 0.f ? x23.y : e23.y;
+  v.x = imin(x01.x, e01.x);
+  v.y = imin(x01.y, e01.y);
+  v.z = imin(x23.x, e23.x);
+  v.w = imin(x23.y, e23.y);
   return v;
 }
 
@@ -1485,7 +1500,31 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
     // no action post-processing (the lean kernel; a general-body program without
     // tanh / clip / scale, e.g. a GRU policy): the head's activation (usually none)
     // and the plain store of the valid rows / columns, from the hot fields
-    if (!CTL && (PL || hot.post_plain)) {
+    if constexpr (!CTL && PL) {
+      // the lean kernel: one store sequence; the head's activation (identity for the
+      // exported policies) applied per element only when there is one. (with_act here
+      // compiled the store once per activation kind: a branch ladder and the address
+      // arithmetic from SGPRs spilled to VGPR lanes, ~660 cycles from the partial sums
+      // to the store, profiles/r05_clock_mlp512.json tail_store.)
+      const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
+      float4 v = make_float4(hs[0][0] + hbv[0].x, hs[0][1] + hbv[0].y, hs[0][2] + hbv[0].z, hs[0][3] + hbv[0].w);
+      if (hot.head_act != 0) {
+        v.x = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.x);
+        v.y = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.y);
+        v.z = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.z);
+        v.w = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.w);
+      }
+      if (row < B) {  // (ac = the action rows of all steps, this step's at step * B rows)
+        float *o = ac + ((size_t)step * B + row) * hot.head_n;
+        if ((hot.head_n & 3) == 0 && ((uintptr_t)ac & 15) == 0) {  // (12 actions: one 16-byte store per lane)
+          if (n0 < hot.head_n) *reinterpret_cast<float4 *>(o + n0) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n0 + r < hot.head_n) o[n0 + r] = f4c(v, r);
+        }
+      }
+    } else if (!CTL && hot.post_plain) {
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
       with_act(hot.head_act, [&](auto act_k) {
         constexpr int ACT = decltype(act_k)::value;
@@ -1507,20 +1546,25 @@ __device__ __forceinline__ void w4_step(const DevProgram &P, const W4Hot &hot0, 
       // head's fields were read with the hot block, before the tile's observation rows
       // went out. (dense_store read them here: vector loads queued behind those 6 KB of
       // row stores, so the action stores waited for all of them.)
+      // (one store sequence, the head's activation per element only when there is one:
+      // as the lean kernel's tail above)
       const int row = row0 + (lane & 15), n0 = wave * 16 + ((lane >> 4) << 2);
-      with_act(hot.head_act, [&](auto act_k) {
-        constexpr int ACT = decltype(act_k)::value;
-        const float4 v = w4_epi<ACT>(ActP{hot.head_act, hot.head_alpha, hot.head_beta}, hs[0], hbv[0]);
-        if (row < B) {
-          if (hot.head_n == GO2PI_CTL_DOF) {
-            if (n0 < GO2PI_CTL_DOF) ctl_store4(cv, row, n0, {v.x, v.y, v.z, v.w});
-          } else {
+      float4 v = make_float4(hs[0][0] + hbv[0].x, hs[0][1] + hbv[0].y, hs[0][2] + hbv[0].z, hs[0][3] + hbv[0].w);
+      if (hot.head_act != 0) {
+        v.x = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.x);
+        v.y = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.y);
+        v.z = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.z);
+        v.w = act_fn(hot.head_act, hot.head_alpha, hot.head_beta, v.w);
+      }
+      if (row < B) {
+        if (hot.head_n == GO2PI_CTL_DOF) {
+          if (n0 < GO2PI_CTL_DOF) ctl_store4(cv, row, n0, {v.x, v.y, v.z, v.w});
+        } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n0 + r < hot.head_n) ctl_store(cv, row, n0 + r, f4c(v, r));
-          }
+          for (int r = 0; r < 4; ++r)
+            if (n0 + r < hot.head_n) ctl_store(cv, row, n0 + r, f4c(v, r));
         }
-      });
+      }
     } else {
       float4 none[1];
       dense_store<1>(P, P.L[nh], hs, hbv, wave, HT, lane, true, nullptr, 0, ac, cv, row0, B, none);

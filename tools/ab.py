@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--workload", default="go2_mlp_512_b4096")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ab"))
+    ap.add_argument("--ctl", action="store_true",
+                    help="compare the controller tick (controller_tick.tick_us, 4096 robots) instead of kernel_us")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     vs = [parse(v) for v in args.variants]
@@ -45,19 +47,23 @@ def main():
         for name, path, env in vs:
             e = dict(os.environ, GO2PI_LIB=path, **env)
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", args.workload, "--steps",
-                   str(args.steps), "--no-cpu", "--no-latency", "--no-ctl", "--no-gru"]
+                   str(args.steps), "--no-cpu", "--no-latency", "--no-gru"] + ([] if args.ctl else ["--no-ctl"])
             p = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(f"{name}: bench failed\n{p.stderr[-2000:]}", flush=True)
                 sys.exit(1)
             d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-            res[name].append(d["kernel_us"])
-            print(f"round {r} {name:12s} {d['kernel_us']:8.3f} us  frac {d['roofline']['frac']:.4f}  {d['kernel']}",
-                  flush=True)
+            if args.ctl:
+                res[name].append(d["controller_tick"]["tick_us"])
+                print(f"round {r} {name:12s} tick {d['controller_tick']['tick_us']:8.3f} us", flush=True)
+            else:
+                res[name].append(d["kernel_us"])
+                print(f"round {r} {name:12s} {d['kernel_us']:8.3f} us  frac {d['roofline']['frac']:.4f}  {d['kernel']}",
+                      flush=True)
     summary = {n: {"min": min(v), "median": statistics.median(v), "all": v} for n, v in res.items()}
     for n, s in summary.items():
         print(f"{n:12s} min {s['min']:8.3f}  median {s['median']:8.3f}")
-    with open(os.path.join(args.out, f"ab_{args.workload}.json"), "w") as fh:
+    with open(os.path.join(args.out, f"ab_{args.workload}{'_ctl' if args.ctl else ''}.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
 
 

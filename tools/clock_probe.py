@@ -112,6 +112,18 @@ def main():
     cyc = st[:, 2] - st[:, 0]
     rt = (st[:, 3] - st[:, 1]) / 100e6
     clk = cyc / rt
+    # per XCD (workgroups are dispatched round-robin over the 8 XCDs: blockIdx % 8): where
+    # the start and end spreads come from (late starts, slower clocks, longer lives)
+    t0s = st[:, 1].min()
+    per_xcd = {}
+    for x in range(8):
+        m = np.arange(st.shape[0]) % 8 == x
+        if m.any():
+            per_xcd[x] = {"start_us_med": float(np.median(st[m, 1] - t0s) / 100),
+                          "start_us_max": float((st[m, 1] - t0s).max() / 100),
+                          "end_us_med": float(np.median(st[m, 3] - t0s) / 100),
+                          "end_us_max": float((st[m, 3] - t0s).max() / 100),
+                          "cycles_med": float(np.median(cyc[m])), "clk_ghz_med": float(np.median(clk[m]) / 1e9)}
     out = {"lib": os.path.basename(os.environ.get("GO2PI_LIB", "default")), "waves": args.waves,
            "launches": n, "clock_ghz_median": float(np.median(clk) / 1e9),
            "clock_ghz_min": float(clk.min() / 1e9), "wg_cycles_median": float(np.median(cyc)),
@@ -123,7 +135,7 @@ def main():
            "phase_cycles_median": phases,
            "layer1_wave_marks": waves_l1,  # [entry, contraction done, epilogue done, barrier] cycles
            "pipeline_layer1_subphases": sub_l1, "init_subphases": init_sub, "gru_stage": gru_sub,
-           "ctl_assembly_blocks": blocks}
+           "ctl_assembly_blocks": blocks, "per_xcd": per_xcd}
     print(json.dumps(out))
 
 
