@@ -1591,6 +1591,7 @@ template <int TPW, int HT, int C0M, int ACTC, int NHC, int NW = 4>
 __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *__restrict__ obs,
                                               float *__restrict__ act, const float *l0w, const float *bpack, int B,
                                               int steps, unsigned dims, unsigned *yield) {
+  GO2PI_ENTRY_CLOCK();
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   // tell idle resident kernels on this device to give their CUs back (resident.hip)
@@ -1623,8 +1624,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
                                          (lvoid_t *)(bufA + r * S + c * 64), 4, 0, 0);
     }
     if (step == 0 && tid < NW) flags[tid] = 0;
-    GO2PI_STAMP(P, tid == 0 && step == 0, 0);
-    GO2PI_STAMP_RT(P, tid == 0 && step == 0, 1);
+    GO2PI_STAMP_ENTRY(P, tid == 0 && step == 0);
     GO2PI_STAMP(P, tid == 0 && step == 0, 40);
     GO2PI_STAMP(P, tid == 0 && step == 0, 41);
     w4_step<TPW, HT, false, true, C0M, ACTC, NHC, NW>(P, hot, bufA, bufB, S, scratch, flags, lbias, ep, wave, lane, act, CtlView{}, row0, B, DevCtl{},
@@ -1649,6 +1649,7 @@ __device__ __forceinline__ void w4_plain_body(const DevProgram &P, const float *
 template <int TPW, int HT, int C0M>
 __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &ctl, const float *l0w,
                                             const float *bpack, unsigned shape, unsigned *yield, int c0) {
+  GO2PI_ENTRY_CLOCK();
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   const int B = (int)(shape & 0xFFFFFu), in_dim = (int)(shape >> 20);
@@ -1669,8 +1670,7 @@ __device__ __forceinline__ void w4_ctl_body(const DevProgram &P, const DevCtl &c
   // behind the staging loads
   if (blockIdx.x == 0 && tid == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  GO2PI_STAMP(P, tid == 0, 0);
-  GO2PI_STAMP_RT(P, tid == 0, 1);
+  GO2PI_STAMP_ENTRY(P, tid == 0);
   GO2PI_STAMP(P, tid == 0, 41);
   const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, c0, 0, 0, 0.f, 0.f, 1, 0.f, 0.f, in_dim};
   const CtlView cv = ctl_view(ctl, CL, row0);
@@ -1702,6 +1702,7 @@ template <int TPW, int HT, int GT, bool LSTM = false>
 __device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *obs, float *act, float *hidden,
                                             const float *gw, const float *l0w, const float *bpack, unsigned shape,
                                             const float *gbzr, const float *gbh, int steps, unsigned *yield) {
+  GO2PI_ENTRY_CLOCK();
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   constexpr int H = 64 * GT, S = 64 * TPW + 4, NBIAS = 3 * 64 * TPW;
@@ -1751,8 +1752,7 @@ __device__ __forceinline__ void w4_gru_body(const DevProgram &P, const float *ob
   if (tid < 4) flags[tid] = 0;
   if (blockIdx.x == 0 && tid == 0 && gridDim.x > GO2PI_YIELD_MIN_GRID)
     __hip_atomic_fetch_add(yield, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  GO2PI_STAMP(P, tid == 0, 0);
-  GO2PI_STAMP_RT(P, tid == 0, 1);
+  GO2PI_STAMP_ENTRY(P, tid == 0);
   const DevGru G{gw, gbzr, gbh, in_dim, ipad, H, LSTM ? 0 : 1, LSTM ? 1 : 0, SW};
   const W4Hot hot = W4Hot{l0w, nullptr, nullptr, bpack, nullptr, NBIAS, 0, H / 16, 0, 0, 0.f, 0.f, 1, 0.f, 0.f};
   // LSTM: this lane's cell-state units, in registers for every tick (rows past B: zeros)
@@ -1798,6 +1798,7 @@ template <int NW, bool CTL, int W4T = 0, int W4H = 0, int C0M = 0, int RNN = 0, 
 __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__restrict__ obs,
                                            float *__restrict__ act, float *__restrict__ hidden, int B, int steps,
                                            const DevCtl ctl) {
+  GO2PI_ENTRY_CLOCK();
   extern __shared__ float4 lds4[];
   float *lds = reinterpret_cast<float *>(lds4);
   const int S = P.lds_stride;
@@ -1847,8 +1848,7 @@ __device__ __forceinline__ void fused_body(const DevProgram &P, const float *__r
   }
   // init sub-phases: 40 descriptors warm, 41 observation loads issued, 42 pipeline barrier reached
   GO2PI_STAMP(P, tid == 0, 40);
-  GO2PI_STAMP(P, tid == 0, 0);
-  GO2PI_STAMP_RT(P, tid == 0, 1);
+  GO2PI_STAMP_ENTRY(P, tid == 0);
 
   // controller tick: this tile's raw inputs staged in LDS behind the scratch
   // region (one burst of direct-to-LDS loads), then assembled from there

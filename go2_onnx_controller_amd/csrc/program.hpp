@@ -45,7 +45,28 @@
       ((__attribute__((address_space(1))) unsigned long long *)(P).stamps)[blockIdx.x * GO2PI_STAMPS_PER_WG + (slot)] = \
           __builtin_amdgcn_s_memrealtime();                                                                  \
   } while (0)
+// (r06) the workgroup's start, taken at kernel entry and stored as slots 0 / 1 once the
+// stamp row is known: a start stamp taken where the row pointer is first read waits for
+// that program load (~1K cycles into a cold launch), which moved that time out of the
+// measured workgroup life and into "event - span"
+#define GO2PI_ENTRY_CLOCK()                                                   \
+  const unsigned long long go2pi_t_entry = __builtin_amdgcn_s_memtime(),     \
+                           go2pi_rt_entry = __builtin_amdgcn_s_memrealtime()
+#define GO2PI_STAMP_ENTRY(P, cond)                                                                       \
+  do {                                                                                                   \
+    if ((P).stamps && (cond)) {                                                                          \
+      auto *r_ = (__attribute__((address_space(1))) unsigned long long *)(P).stamps + blockIdx.x * GO2PI_STAMPS_PER_WG; \
+      r_[0] = go2pi_t_entry;                                                                             \
+      r_[1] = go2pi_rt_entry;                                                                            \
+    }                                                                                                    \
+  } while (0)
 #else
+#define GO2PI_ENTRY_CLOCK() \
+  do {                      \
+  } while (0)
+#define GO2PI_STAMP_ENTRY(P, cond) \
+  do {                             \
+  } while (0)
 #define GO2PI_STAMP_AT(row, cond, slot) \
   do {                                  \
     (void)sizeof(row);                  \
