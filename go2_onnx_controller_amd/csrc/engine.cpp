@@ -188,7 +188,11 @@ namespace {
 void res_register(go2pi_engine *e);
 unsigned *yield_word(int device);
 void res_unregister(go2pi_engine *e);
-void evict_residents(const go2pi_engine *self, int64_t batch);
+std::unique_lock<std::mutex> evict_residents(const go2pi_engine *self, int64_t batch);
+// The process-wide registry of engines that may hold a resident kernel, and the lock
+// that orders a batched launch's eviction + enqueue against every resident relaunch
+// (evict_residents, resident_start)
+std::mutex g_res_mu;
 }  // namespace
 
 struct go2pi_engine {
@@ -234,8 +238,6 @@ struct go2pi_engine {
   bool resident1_ctl = false; // controller form in one workgroup (512 threads)
   bool wide = false;          // act() form for wide policies (resident_wide.hip policy_wide_kernel, r06)
   int64_t res_launches = 0;   // resident kernel launches (go2pi_resident_launches)
-  bool no_evict = false;      // GO2PI_RES_NO_EVICT=1 at create: this engine's batched launches evict no resident
-                              // kernel of another engine (A/B diagnostics; tests/test_gpu_resident.py)
   bool ctl_gran_ok = false;   // ... answered in granules (policy_act1_kernel, r05): no done word per tick
   std::vector<float> res_rows = std::vector<float>(GO2PI_SMALL_MAXB * (GO2PI_CTL_RAW + 16 * GO2PI_CTL_STEP_DIM));
   unsigned long long *h_req = nullptr, *m_req = nullptr;  // request granules: host view, device view
@@ -346,6 +348,8 @@ struct go2pi_engine {
     hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize (resident kernel leaving)");
   }
   void resident_start(const go2pi::DevCtl *ctl) {
+    // (never between another thread's eviction and its batched launch: evict_residents)
+    std::lock_guard<std::mutex> res_lk(g_res_mu);
     const size_t ng = (size_t)std::max(1, prog.nl - 1) * gstride;
     hip_check(hipMemsetAsync(d_gran, 0, ng * sizeof(unsigned long long), stream), "hipMemsetAsync");
     hip_check(hipMemsetAsync(d_mirror, 0, sizeof(unsigned long long) * (1 + GO2PI_SMALL_MAXB * (size_t)model.in_dim),
@@ -638,8 +642,7 @@ namespace {
 // rounds: measured 37.8 -> 71.4 us per 4096-robot step (tools/interference.py,
 // DESIGN §4.2b). So every batched launch first tells the other engines' live
 // resident kernels on its device to leave (a LEAVE header; no wait), and their
-// next act() relaunches. GO2PI_RES_NO_EVICT=1 keeps them (A/B diagnostics).
-std::mutex g_res_mu;
+// next act() relaunches.
 std::vector<go2pi_engine *> g_res_engines;
 
 void res_register(go2pi_engine *e) {
@@ -671,12 +674,18 @@ unsigned *yield_word(int device) {
 // batch: the rows of the launch that follows (one 16-row workgroup each); a launch of
 // at most GO2PI_YIELD_MIN_GRID workgroups fits beside the resident kernels and evicts
 // none (the kernels' own yield bump has the same bound, program.hpp).
-void evict_residents(const go2pi_engine *self, int64_t batch) {
-  if (self->no_evict || (batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS <= GO2PI_YIELD_MIN_GRID) return;
-  std::lock_guard<std::mutex> lk(g_res_mu);
+// The lock comes back held: the caller keeps it until its batched launch is enqueued.
+// A resident kernel another thread relaunched in between (resident_start takes the same
+// lock) could otherwise sit ahead of that launch in a hardware queue two streams share,
+// and serve its own requests until it idles out while the launch waits behind it (it
+// leaves on the launch's yield bump only once the launch has started).
+std::unique_lock<std::mutex> evict_residents(const go2pi_engine *self, int64_t batch) {
+  if ((batch + GO2PI_TILE_ROWS - 1) / GO2PI_TILE_ROWS <= GO2PI_YIELD_MIN_GRID) return {};
+  std::unique_lock<std::mutex> lk(g_res_mu);
   for (go2pi_engine *o : g_res_engines)
     if (o != self && o->device == self->device && o->res_flag.load() == 1)
       __atomic_store_n(o->h_req, (unsigned long long)GO2PI_RES_LEAVE << 32, __ATOMIC_SEQ_CST);
+  return lk;
 }
 
 // K is padded to a multiple of 64 (4 chunks: the kernel's unroll); a hidden layer's
@@ -1090,7 +1099,6 @@ void build(go2pi_engine &e, const uint8_t *bytes, size_t n, const go2pi_opts *o)
   e.resident1 = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, false) && !std::getenv("GO2PI_RES_MULTI");
   e.resident1_ctl = e.resident_ok && !m.has_gru && go2pi::resident1_fits(p, true) && !std::getenv("GO2PI_RES_MULTI");
   e.ctl_gran_ok = e.resident1_ctl && go2pi::resident1_ctl_granules(p);
-  e.no_evict = std::getenv("GO2PI_RES_NO_EVICT") != nullptr;
   // the controller tick's general body instead of the lean tick kernel (A/B diagnostics,
   // tests/test_gpu_controller.py::test_controller_tick_bodies)
   p.ctl_general = std::getenv("GO2PI_CTL_GENERAL") != nullptr ? 1 : 0;
@@ -1304,7 +1312,8 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
       return GO2PI_OK;
     }
     e->resident_stop();
-    if (batch > GO2PI_SMALL_MAXB || !e->latency_ok) evict_residents(e, batch);  // a batched (fused) launch follows
+    std::unique_lock<std::mutex> ev;  // (held until the launch below is enqueued)
+    if (batch > GO2PI_SMALL_MAXB || !e->latency_ok) ev = evict_residents(e, batch);  // a batched (fused) launch follows
     const size_t in_b = sizeof(float) * (size_t)batch * e->model.in_dim;
     const size_t out_b = sizeof(float) * (size_t)batch * e->model.out_dim;
     if (batch <= GO2PI_SMALL_MAXB) {
@@ -1321,12 +1330,14 @@ int go2pi_run(go2pi_engine *e, const float *obs, float *act, int64_t batch) {
       } else {
         hip_check(hipGraphLaunch(e->graph_for((int)batch), e->stream), "hipGraphLaunch");
       }
+      if (ev.owns_lock()) ev.unlock();  // (the launch is enqueued)
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
       e->check_handoff();
       std::memcpy(act, e->h_act, out_b);
     } else {
       hip_check(hipMemcpyAsync(e->d_obs, obs, in_b, hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync H2D");
       e->enqueue(e->d_obs, e->d_act, batch, e->stream);
+      if (ev.owns_lock()) ev.unlock();  // (the launch is enqueued)
       hip_check(hipMemcpyAsync(act, e->d_act, out_b, hipMemcpyDeviceToHost, e->stream), "hipMemcpyAsync D2H");
       hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
       e->check_handoff();
@@ -1343,7 +1354,8 @@ int go2pi_run_device(go2pi_engine *e, const float *obs_dev, float *act_dev, int6
     if (!obs_dev || !act_dev) throw ApiError("null obs/act buffer", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     e->check_handoff();  // a failure of an earlier asynchronous launch surfaces here (or at go2pi_sync)
-    if (!e->use_latency(batch)) evict_residents(e, batch);
+    std::unique_lock<std::mutex> ev;  // (held until the launch is enqueued)
+    if (!e->use_latency(batch)) ev = evict_residents(e, batch);
     e->enqueue(obs_dev, act_dev, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;
   });
@@ -1361,7 +1373,7 @@ int go2pi_run_sequence_device(go2pi_engine *e, const float *obs_dev, float *act_
       throw ApiError("sequence too large", GO2PI_E_INVALID);
     hip_check(hipSetDevice(e->device), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    evict_residents(e, batch);
+    const auto ev = evict_residents(e, batch);  // (held until the launch is enqueued)
     hip_check(go2pi::launch_policy_fused(e->prog, e->d_prog, e->waves, obs_dev, act_dev, e->d_hidden, (int)batch,
                                          (int)steps, s),
               "fused sequence launch");
@@ -1621,8 +1633,10 @@ int go2pi_controller_step(go2pi_engine *e, const float *state, const float *joy,
       e->resident_stop();
     }
     const bool single = !served && small && e->use_latency(batch) && e->done_ok;
-    if (!single && !served) evict_residents(e, batch);  // a batched (fused) launch follows
+    std::unique_lock<std::mutex> ev;
+    if (!single && !served) ev = evict_residents(e, batch);  // a batched (fused) launch follows
     if (!served) e->enqueue_ctl(c, batch, e->stream, single ? e->m_done : nullptr);
+    if (ev.owns_lock()) ev.unlock();  // (the launch is enqueued)
     if (small) {
       const bool synced = served || (single && e->spin_done());
       if (!synced) hip_check(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
@@ -1664,7 +1678,8 @@ int go2pi_controller_step_device(go2pi_engine *e, const float *state, const floa
     // a live resident kernel shares the granules, epoch and error words the batch <= 8
     // launch uses: it leaves first (as for every other call on the engine)
     e->resident_stop();
-    if (!(e->use_latency(batch) && e->done_ok)) evict_residents(e, batch);
+    std::unique_lock<std::mutex> ev;  // (held until the launch is enqueued)
+    if (!(e->use_latency(batch) && e->done_ok)) ev = evict_residents(e, batch);
     go2pi::DevCtl c{e->d_ctl, state, joy, obs, action, q_des, kp, kd, status};
     e->enqueue_ctl(c, batch, static_cast<hipStream_t>(hip_stream));
     return GO2PI_OK;

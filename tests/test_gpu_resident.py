@@ -514,50 +514,6 @@ def test_batched_launch_evicts_other_resident_kernels(synth_path):
     assert n_act[0] > 10
 
 
-def test_no_evict_switch(synth_path, monkeypatch):
-    """GO2PI_RES_NO_EVICT=1 at create: the batched engine's 4096-robot launches leave the
-    other engine's resident kernel live (A/B of DESIGN §4.2b); both stay correct, the
-    resident act() from another thread and the batched results."""
-    import threading
-    import torch
-    from go2_onnx_controller_amd import Engine
-    from oracle import mlp_ref
-    monkeypatch.setenv("GO2PI_RES_NO_EVICT", "1")
-    pb = synth_path("go2_mlp_512")
-    ra, rb = mlp_ref.MlpRef.from_onnx(SHIPPED), mlp_ref.MlpRef.from_onnx(pb)
-    errs, n_act = [], [0]
-    stop = threading.Event()
-    with Engine(SHIPPED, max_batch=8, resident_ms=1000) as a, Engine(pb, max_batch=4096) as b:
-        x1 = realistic_obs(1, seed=6)
-        want1 = ra.f64(x1)
-        a.run(x1)
-
-        def tick():
-            try:
-                while not stop.is_set():
-                    if abs_err(a.run(x1), want1) > TOL:
-                        errs.append("act() output changed")
-                    n_act[0] += 1
-                    time.sleep(0.001)
-            except Exception as ex:  # noqa: BLE001 - reported below
-                errs.append(repr(ex))
-        th = threading.Thread(target=tick)
-        th.start()
-        try:
-            xb = torch.randn((4096, 48), device="cuda:0")
-            s = torch.cuda.Stream()
-            for _ in range(20):
-                yb = b.run_torch(xb, stream=s)
-                s.synchronize()
-                time.sleep(0.002)
-            assert abs_err(yb.cpu().numpy(), rb.f64(xb.cpu().numpy())) <= TOL
-        finally:
-            stop.set()
-            th.join(timeout=10)
-    assert not errs, errs
-    assert n_act[0] > 10
-
-
 def test_diag_stamps_switch(synth_path, monkeypatch):
     """GO2PI_DIAG_STAMPS=1 at create allocates the diagnostics stamp buffer the clock /
     timeline builds write; in the product build nothing writes it, and every path stays
