@@ -197,7 +197,11 @@ __device__ __forceinline__ float ctl_pro(const CtlQ &q, float x, int k) {
 // nanm: bit r set when a value of row r is NaN (OR-ed into L.nanf once per thread by
 // ctl_nan_flush: a workgroup-scope LDS atomic per element, on the few addresses of 16
 // rows, serialised in the LDS pipeline).
-template <int BK, bool TILE, bool ARITH>
+// ONE (r06): nrows * d <= nt (the batched tile: 16 rows, 256 threads), so each thread
+// has at most one element of the block: straight-line predicated code instead of a loop,
+// and the caller's seven blocks become one sequence the compiler can schedule as a whole
+// (their LDS reads in flight together).
+template <int BK, bool TILE, bool ARITH, bool ONE = false>
 __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, bool joy, int nrows,
                                                  float *__restrict__ dst, int ds, float *__restrict__ raw, int tid,
                                                  int nt, unsigned &nanm) {
@@ -212,7 +216,7 @@ __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, 
   int t = tid - (64 * BK) % nt;
   if (t < 0) t += nt;
   if constexpr (BK == 0) {  // gravity: a quad of lanes per robot (ctl_gravity_quad; nt % 4 == 0)
-    for (int e = t; e < nrows * 4; e += nt) {
+    for (int e = t; e < nrows * 4; e += ONE ? 1 << 30 : nt) {
       const int r = e >> 2, c = e & 3, k = k0 + c;
 #if defined(GO2PI_DIAG_GRAV_TRIVIAL)  // (diagnostics: the block's cost without its arithmetic)
       const float x = st_l[r * GO2PI_CTL_STATE_DIM + c];
@@ -227,7 +231,7 @@ __device__ __forceinline__ void ctl_append_block(const CtlLds L, const CtlQ &q, 
     }
     return;
   }
-  for (int e = t; e < nrows * d; e += nt) {
+  for (int e = t; e < nrows * d; e += ONE ? 1 << 30 : nt) {
     const int r = e / d, c = e - r * d, k = k0 + c;
     const float *st = st_l + r * GO2PI_CTL_STATE_DIM;
     float x;
@@ -271,16 +275,16 @@ __device__ __forceinline__ void ctl_nan_flush(const CtlLds L, unsigned nanm) {
 // The appended blocks that read no previous observation row (all but vel_cmd, block 2,
 // which keeps the previous command without a joystick): they can run while the
 // previous rows are still in flight (ctl_assemble_split).
-template <bool TILE, bool ARITH>
+template <bool TILE, bool ARITH, bool ONE = false>
 __device__ __forceinline__ void ctl_append_noobs(const CtlLds L, const CtlQ &q, bool joy, int nrows,
                                                  float *__restrict__ dst, int ds, float *__restrict__ raw, int tid,
                                                  int nt, unsigned &nanm) {
-  ctl_append_block<0, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
-  ctl_append_block<1, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
-  ctl_append_block<3, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
-  ctl_append_block<4, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
-  ctl_append_block<5, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
-  ctl_append_block<6, TILE, ARITH>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<0, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<1, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<3, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<4, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<5, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+  ctl_append_block<6, TILE, ARITH, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
 }
 
 template <bool TILE, bool ARITH>
@@ -355,14 +359,13 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nro
     }
   }
   if constexpr (TILE && PAD) {
-    const int pw = q.in_pad - in_dim;
-    for (int e = tid; e < nrows * pw; e += nt) {
-      const int r = e / pw;
-      dst[r * ds + in_dim + (e - r * pw)] = 0.f;
-    }
-    for (int e = tid; e < (GO2PI_TILE_ROWS - nrows) * q.in_pad; e += nt) {
-      const int r = nrows + e / q.in_pad;
-      dst[r * ds + (e - (r - nrows) * q.in_pad)] = 0.f;
+    // sixteen threads per row, no division (r06: the two division loops this replaces
+    // compiled to ~700 instructions of unrolled remainder handling): a row's padding
+    // columns [in_dim, in_pad), every column of a row past nrows
+    const int in_pad = q.in_pad;
+    for (int i = tid; i < GO2PI_TILE_ROWS * 16; i += nt) {
+      const int r = i >> 4;
+      for (int c = (r < nrows ? in_dim : 0) + (i & 15); c < in_pad; c += 16) dst[r * ds + c] = 0.f;
     }
   }
 }
@@ -409,16 +412,18 @@ __device__ __forceinline__ void ctl_assemble_split(const DevProgram &P, const Ct
                                                    int nrows, float *dst, int ds, float *raw, int tid, int nt,
                                                    MID &&mid) {
   unsigned nanm = 0u;
+  // (the batched tile: 16 rows over 256 threads, at most one element of a block per thread)
+  constexpr bool ONE = true;
   if (TILE && (q.pro.sub || q.pro.div || q.pro.mul)) {
-    ctl_append_noobs<TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    ctl_append_noobs<TILE, true, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     mid();
-    ctl_append_block<2, TILE, true>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    ctl_append_block<2, TILE, true, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     GO2PI_STAMP(P, tid == 0, 50);
     ctl_shift<TILE, true, 4>(L, q, nrows, dst, ds, raw, tid, nt);
   } else {
-    ctl_append_noobs<TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    ctl_append_noobs<TILE, false, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     mid();
-    ctl_append_block<2, TILE, false>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
+    ctl_append_block<2, TILE, false, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     GO2PI_STAMP(P, tid == 0, 50);
     ctl_shift<TILE, false, 4>(L, q, nrows, dst, ds, raw, tid, nt);
   }
