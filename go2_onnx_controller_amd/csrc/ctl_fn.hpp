@@ -370,6 +370,54 @@ __device__ __forceinline__ void ctl_shift(const CtlLds L, const CtlQ &q, int nro
   }
 }
 
+// ctl_shift for the batched tile (r06): a thread per (shifted column, row group), its
+// column's block, width and source worked out once (ctl_shift derives row, block and
+// source per element), then up to four rows' reads in flight before their writes. The
+// tile's padding as ctl_shift's.
+template <bool ARITH>
+__device__ __forceinline__ void ctl_shift_cols(const CtlLds L, const CtlQ &q, int nrows, float *__restrict__ dst,
+                                               int ds, float *__restrict__ raw, int tid, int nt) {
+  const float *__restrict__ obs_l = L.obs;
+  const int H = q.hist, h1 = H - 1, in_dim = q.in_dim, nc = h1 * GO2PI_CTL_STEP_DIM;
+  if (nc > 0) {
+    const bool fit = nc <= nt;
+    const int G = fit ? nt / nc : 1;  // row groups
+    for (int j0 = 0; j0 < nc; j0 += fit ? nc : nt) {
+      int g = 0, j = j0 + tid;
+      if (fit) {
+        // tid / nc exactly: (tid + 0.5) / nc is >= 0.5 / nc from an integer, far above
+        // the ~1 ulp error of the hardware reciprocal at tid < 1024
+        g = (int)(((float)tid + 0.5f) * __builtin_amdgcn_rcpf((float)nc));
+        j = tid - g * nc;
+      }
+      if (g >= G || j >= nc) continue;
+      const int b = (j >= h1 * 3) + (j >= h1 * 6) + (j >= h1 * 9) + (j >= h1 * 21) + (j >= h1 * 33) + (j >= h1 * 45);
+      const int cum = ctl_cum(b), d = ctl_width(b);
+      const int k = H * cum + (j - h1 * cum);
+      const float *src = obs_l + k + d;
+      int r = g;
+      for (; r < nrows; r += 4 * G) {
+        float x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = r + u * G < nrows ? src[(r + u * G) * in_dim] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int rr = r + u * G;
+          if (rr < nrows) {
+            raw[rr * in_dim + k] = x[u];
+            dst[rr * ds + k] = ctl_pro<true, ARITH>(q, x[u], k);
+          }
+        }
+      }
+    }
+  }
+  const int in_pad = q.in_pad;
+  for (int i = tid; i < GO2PI_TILE_ROWS * 16; i += nt) {
+    const int r = i >> 4;
+    for (int c = (r < nrows ? in_dim : 0) + (i & 15); c < in_pad; c += 16) dst[r * ds + c] = 0.f;
+  }
+}
+
 // Assemble this tick's observation rows r < nrows from the LDS image (needs the
 // image complete: barrier) over all nt threads of the workgroup: the appended
 // values (ctl_append) and the shifted ones (ctl_shift) go to disjoint columns, so
@@ -419,13 +467,15 @@ __device__ __forceinline__ void ctl_assemble_split(const DevProgram &P, const Ct
     mid();
     ctl_append_block<2, TILE, true, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     GO2PI_STAMP(P, tid == 0, 50);
-    ctl_shift<TILE, true, 4>(L, q, nrows, dst, ds, raw, tid, nt);
+    if constexpr (TILE) ctl_shift_cols<true>(L, q, nrows, dst, ds, raw, tid, nt);
+    else ctl_shift<TILE, true, 4>(L, q, nrows, dst, ds, raw, tid, nt);
   } else {
     ctl_append_noobs<TILE, false, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     mid();
     ctl_append_block<2, TILE, false, ONE>(L, q, joy, nrows, dst, ds, raw, tid, nt, nanm);
     GO2PI_STAMP(P, tid == 0, 50);
-    ctl_shift<TILE, false, 4>(L, q, nrows, dst, ds, raw, tid, nt);
+    if constexpr (TILE) ctl_shift_cols<false>(L, q, nrows, dst, ds, raw, tid, nt);
+    else ctl_shift<TILE, false, 4>(L, q, nrows, dst, ds, raw, tid, nt);
   }
   ctl_nan_flush(L, nanm);
   GO2PI_STAMP(P, tid == 0, 51);
